@@ -1,0 +1,161 @@
+/*
+ * vx_hash.h — C ABI of the MI355X SHA-1 piece-verification engine.
+ *
+ * This is the drop-in boundary for vortex's "Parallel hash computations" pool.
+ * In the reference the boundary is not a trait but an inline closure handed to
+ * rayon plus an mpsc channel back to the event loop:
+ *
+ *   submit   bittorrent/src/peer_comm/peer_connection.rs:1145-1158
+ *            scope.spawn(move |_| { Sha1 over buffer[..piece_len];
+ *                                   == metadata.pieces[index];
+ *                                   complete_tx.send(DownloadedPiece{..}) })
+ *   complete bittorrent/src/torrent.rs:415-442
+ *            while let Ok(p) = downloaded_piece_rc.try_recv() { .. }
+ *   bulk     bittorrent/src/torrent.rs:724-740 (par_iter over all pieces,
+ *            each bittorrent/src/file_store.rs:228-303 check_piece_hash_sync)
+ *   record   bittorrent/src/piece_selector.rs:311-317 (DownloadedPiece)
+ *
+ * Every entry point below names the reference interface it replaces.  The
+ * signatures use only plain pointers, sizes and integers so that Rust
+ * (`extern "C"`), ctypes, cgo or JNI can bind them directly; INTEGRATION.md
+ * shows the Rust binding.
+ *
+ * Conventions
+ *  - Return codes are 0 on success or a negative errno-style VX_E* value.  A
+ *    hash mismatch is NOT an error: it is reported as matched = 0, exactly as
+ *    the reference reports hash_matched = false.  No function aborts or throws
+ *    across the ABI; vx_last_error() gives a thread-local message.
+ *  - Digests are the 20-byte big-endian SHA-1 output (what
+ *    `Sha1::finalize().as_slice()` returns), stored back to back.
+ *  - Threading (mirrors the reference): one thread (the io_uring event-loop
+ *    thread) submits and the same thread polls.  A vx_ctx is not internally
+ *    synchronised; internal HIP streams are invisible to the caller.
+ *  - Device entry points (vx_sha1_device_*) take device pointers and a HIP
+ *    stream (hipStream_t passed as void*; NULL = the null stream) and only
+ *    enqueue work: they return before the kernel finishes.
+ */
+#ifndef VX_HASH_H
+#define VX_HASH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VX_ABI_VERSION 1
+
+/* Error codes (negative errno values). */
+#define VX_OK 0
+#define VX_EINVAL (-22)  /* bad argument (null pointer, n/len out of range, misalignment) */
+#define VX_ENOMEM (-12)  /* host or device allocation failed */
+#define VX_ERANGE (-34)  /* piece longer than the context's max_piece_len */
+#define VX_ENODEV (-19)  /* no such HIP device */
+#define VX_EDEVICE (-5)  /* a HIP runtime call failed (see vx_last_error) */
+#define VX_EBUSY (-16)   /* operation not allowed while work is in flight */
+
+#define VX_DIGEST_LEN 20
+
+/* Device batch layout: piece bytes live in one device allocation; piece i
+ * starts at base + offsets[i] (uniform batches: base + i*stride).  Piece
+ * starts must be 16-byte aligned (the kernels load 16 bytes per lane);
+ * lengths are arbitrary (0 .. 4 GiB-1). */
+
+/* One completion, the C form of DownloadedPiece (piece_selector.rs:311-317):
+ * `tag` is whatever the caller passed to vx_submit (vortex packs the piece
+ * index and the ConnectionId into it), `matched` is hash_matched.  The Buffer
+ * member has no C counterpart: the caller keeps the buffer and gets it back
+ * by tag. */
+typedef struct vx_completion {
+    uint64_t tag;
+    uint8_t matched;
+    uint8_t digest[VX_DIGEST_LEN];
+    uint8_t _pad[3];
+} vx_completion;
+
+typedef struct vx_config {
+    int32_t device;          /* HIP device ordinal                                   */
+    uint32_t max_piece_len;  /* bytes; torrent piece_length (torrent.rs:344 pool size) */
+    uint32_t batch_pieces;   /* launch a batch once this many pieces are queued      */
+    uint32_t slots;          /* batches in flight (each has its own stream + arena)  */
+    uint64_t slot_bytes;     /* device arena bytes per slot (>= max_piece_len)       */
+} vx_config;
+
+typedef struct vx_ctx vx_ctx;
+
+/* ---- library ---------------------------------------------------------- */
+int vx_abi_version(void);
+const char* vx_last_error(void);
+const char* vx_strerror(int code);
+/* Number of HIP devices (0 when no GPU or no driver). */
+int vx_device_count(void);
+/* Fill *cfg with defaults for a torrent whose piece_length is max_piece_len. */
+void vx_config_default(vx_config* cfg, uint32_t max_piece_len);
+
+/* ---- context: replaces InitializedState's downloaded_piece_tx/rc pair and
+ *      the rayon scope it feeds (torrent.rs:319-320, 333; event_loop.rs:385) */
+int vx_create(const vx_config* cfg, vx_ctx** out);
+/* Drains all in-flight work first (the reference's scope joins every spawned
+ * hash before EventLoop::run returns, event_loop.rs:385-602), then frees. */
+int vx_destroy(vx_ctx* ctx);
+
+/* Pin a host range (e.g. a BufferPool's AnonymousMmap, buf_ring.rs:24-42) so
+ * pieces inside it are DMA'd straight to the GPU instead of being staged
+ * through an internal pinned copy.  Ranges must not overlap. */
+int vx_register_host_buffer(vx_ctx* ctx, void* ptr, size_t len);
+int vx_unregister_host_buffer(vx_ctx* ctx, void* ptr);
+
+/* ---- async download path ---------------------------------------------- */
+/* Replaces `scope.spawn(hash closure)` (peer_connection.rs:1145-1158).
+ * Hashes data[0..len) and compares with expected[0..20).  The engine borrows
+ * `data` until the completion carrying `tag` has been returned by vx_poll;
+ * it never frees or keeps it afterwards.  Never blocks on the GPU unless every
+ * slot is in flight, in which case it waits for the oldest batch (the
+ * reference's spawn never refuses work either). */
+int vx_submit(vx_ctx* ctx, uint64_t tag, const uint8_t* data, uint32_t len, const uint8_t* expected);
+/* Launch whatever is queued (call once per event-loop turn, next to the
+ * drain at event_loop.rs:554-557). */
+int vx_flush(vx_ctx* ctx);
+/* Replaces `downloaded_piece_rc.try_recv()` (torrent.rs:418): non-blocking,
+ * returns how many completions were written to out[0..max).  Order is the
+ * order batches finish, which like the reference is not submission order.
+ * Returns a negative VX_E* if a batch failed on the device. */
+int64_t vx_poll(vx_ctx* ctx, vx_completion* out, size_t max);
+/* Flush and block until every submitted piece has completed (results stay
+ * queued for vx_poll).  timeout_ms = 0 waits forever. */
+int vx_drain(vx_ctx* ctx, uint32_t timeout_ms);
+/* Pieces submitted but not yet returned by vx_poll. */
+uint64_t vx_pending(const vx_ctx* ctx);
+
+/* ---- synchronous host batches (bulk re-verify, torrent.rs:724-740) ----- */
+/* digests_out: n*20 bytes.  Pieces are pipelined through the slots. */
+int vx_sha1_batch(vx_ctx* ctx, const uint8_t* const* ptrs, const uint32_t* lens, size_t n, uint8_t* digests_out);
+/* expected: n*20 bytes; matched_out: n bytes of 0/1 (the Box<[bool]> of
+ * torrent.rs:727-740); digests_out may be NULL. */
+int vx_verify_batch(vx_ctx* ctx, const uint8_t* const* ptrs, const uint32_t* lens, const uint8_t* expected,
+                    size_t n, uint8_t* matched_out, uint8_t* digests_out);
+
+/* ---- device-resident batches (the hot path; no context needed) -------- */
+/* Pieces i in [0,n) at d_base + i*stride, each len bytes.  Writes
+ * d_digests[20*i..] (may be NULL) and, when d_expected is given,
+ * d_matched[i] = (digest == d_expected[20*i..]) (0/1).  stride and d_base
+ * must be multiples of 16 and stride >= len. */
+int vx_sha1_device_uniform(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
+                           const void* d_expected, void* d_matched, void* stream);
+/* Ragged batch: piece i at d_base + d_offsets[i] (16-byte aligned), d_lens[i]
+ * bytes.  d_order (may be NULL) is a permutation of [0,n) telling lane j to
+ * hash piece d_order[j]; pass pieces sorted by descending length so each
+ * wavefront gets equal-length work (see vx_sort_order).  max_len bounds all
+ * lengths (used only to validate). */
+int vx_sha1_device_ragged(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
+                          const uint32_t* d_order, uint32_t n, void* d_digests, const void* d_expected,
+                          void* d_matched, void* stream);
+/* Host helper: write into order_out the permutation that sorts lens[0..n)
+ * by descending length (stable).  Used to build d_order. */
+int vx_sort_order(const uint32_t* lens, uint32_t n, uint32_t* order_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VX_HASH_H */

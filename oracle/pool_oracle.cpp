@@ -1,0 +1,151 @@
+// oracle/pool_oracle.cpp — TEST INFRASTRUCTURE ONLY (CPU restatement of vortex's
+// "Parallel hash computations" pool).  Used as the parity checker in tests/ and
+// as the timed CPU baseline in bench.py (cpu_baseline.kind = "port"); never
+// linked into vortex_amd/.
+//
+// What it restates (reference is Rust + rayon, not buildable here: no cargo):
+//  * Download path: each completed piece is one task on the rayon global pool,
+//    `scope.spawn(move |_| { Sha1::new(); update(&buf[..piece_len]); finalize()
+//    == metadata.pieces[index]; complete_tx.send(DownloadedPiece{..}) })`
+//    — bittorrent/src/peer_comm/peer_connection.rs:1145-1158.
+//  * Results travel over std::sync::mpsc (torrent.rs:319-320, 333) and the
+//    submitting (event-loop) thread drains them with try_recv
+//    (torrent.rs:415-442).
+//  * Bulk re-verify is `pieces.par_iter().enumerate().map(check).collect()`
+//    (torrent.rs:724-740).
+//  * Pool size: rayon's default global pool = one worker per logical CPU; the
+//    reference never overrides it (no ThreadPoolBuilder / RAYON_NUM_THREADS).
+//    Callers pass the thread count explicitly so the bench can report it.
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+extern "C" {
+void vxo_sha1_backend(const uint8_t* data, size_t len, uint8_t out[20], int backend);
+void vxo_gen_piece(uint64_t seed, uint64_t piece, uint32_t len, uint32_t corrupt_every, uint8_t* out);
+}
+
+namespace {
+
+// DownloadedPiece (piece_selector.rs:311-317) minus the Buffer, which the
+// caller keeps: index, hash_matched, plus the digest for bit-exact checks.
+struct DownloadedPiece {
+    size_t index;
+    bool hash_matched;
+    uint8_t digest[20];
+};
+
+// std::sync::mpsc stand-in: unbounded MPSC queue, many senders, one receiver.
+class Mpsc {
+  public:
+    void send(const DownloadedPiece& p) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            q_.push_back(p);
+        }
+        cv_.notify_one();
+    }
+    DownloadedPiece recv() {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return !q_.empty(); });
+        DownloadedPiece p = q_.front();
+        q_.pop_front();
+        return p;
+    }
+
+  private:
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<DownloadedPiece> q_;
+};
+
+template <class Job>
+void run_pool(size_t n, int threads, Job job, Mpsc& tx) {
+    // Work distribution: a shared task counter (each piece is one task, as
+    // with scope.spawn / par_iter; rayon's work stealing degenerates to this
+    // for equal-cost independent tasks).
+    if (threads < 1) threads = 1;
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> ws;
+    ws.reserve(threads);
+    for (int t = 0; t < threads; ++t) {
+        ws.emplace_back([&, t] {
+            (void)t;
+            for (;;) {
+                size_t i = next.fetch_add(1, std::memory_order_relaxed);
+                if (i >= n) break;
+                tx.send(job(i));
+            }
+        });
+    }
+    // The submitting thread drains the channel (torrent.rs:415-442).
+    for (size_t got = 0; got < n; ++got) (void)got, tx.recv();
+    for (auto& w : ws) w.join();
+}
+
+}  // namespace
+
+extern "C" {
+
+// Verify n host-resident pieces.  expected: n*20 bytes (nullable → matched
+// left untouched); digests_out: n*20 bytes (nullable).  Returns 0.
+int vxo_pool_verify(const uint8_t* const* ptrs, const uint32_t* lens, const uint8_t* expected, size_t n,
+                    int threads, int backend, uint8_t* matched_out, uint8_t* digests_out) {
+    Mpsc ch;
+    std::vector<DownloadedPiece> results(n);
+    auto job = [&](size_t i) {
+        DownloadedPiece p;
+        p.index = i;
+        vxo_sha1_backend(ptrs[i], lens[i], p.digest, backend);
+        p.hash_matched = expected ? std::memcmp(p.digest, expected + 20 * i, 20) == 0 : false;
+        results[i] = p;  // disjoint slots; also sent through the channel below
+        return p;
+    };
+    run_pool(n, threads, job, ch);
+    for (size_t i = 0; i < n; ++i) {
+        if (matched_out) matched_out[i] = results[i].hash_matched ? 1 : 0;
+        if (digests_out) std::memcpy(digests_out + 20 * i, results[i].digest, 20);
+    }
+    return 0;
+}
+
+// Same pool over synthetic pieces [first, first+n) generated per task into a
+// per-thread buffer, so 16 GiB batches can be checked without holding them in
+// host memory.  Piece i has length piece_len, except global index
+// last_index (if < UINT64_MAX) which has last_len (piece_selector.rs:291-298).
+int vxo_pool_digest_synth(uint64_t seed, uint64_t first, size_t n, uint32_t piece_len, uint64_t last_index,
+                          uint32_t last_len, uint32_t corrupt_every, int threads, int backend,
+                          uint8_t* digests_out) {
+    Mpsc ch;
+    if (threads < 1) threads = 1;
+    std::vector<std::vector<uint8_t>> bufs(threads);
+    std::atomic<int> slot{0};
+    thread_local int my_slot = -1;
+    thread_local const void* my_owner = nullptr;
+    auto job = [&](size_t i) {
+        if (my_owner != &bufs) {
+            my_slot = slot.fetch_add(1);
+            my_owner = &bufs;
+        }
+        std::vector<uint8_t>& b = bufs[my_slot];
+        uint64_t g = first + i;
+        uint32_t len = (g == last_index) ? last_len : piece_len;
+        if (b.size() < len) b.resize(len);
+        vxo_gen_piece(seed, g, len, corrupt_every, b.data());
+        DownloadedPiece p;
+        p.index = i;
+        p.hash_matched = false;
+        vxo_sha1_backend(b.data(), len, p.digest, backend);
+        std::memcpy(digests_out + 20 * i, p.digest, 20);
+        return p;
+    };
+    run_pool(n, threads, job, ch);
+    return 0;
+}
+
+}  // extern "C"

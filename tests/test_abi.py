@@ -1,0 +1,107 @@
+"""CPU: the C-ABI library builds, loads and exports every symbol the headers
+declare; argument validation works without a GPU (no compute calls)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+
+def declared_symbols():
+    names = set()
+    for h in ("vx_hash.h", "vx_synth.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(vx_[a-z0-9_]+)\s*\(", src))
+    return names
+
+
+def test_headers_compile_as_c(tmp_path):
+    c = tmp_path / "t.c"
+    c.write_text('#include "vx_hash.h"\n#include "vx_synth.h"\nint main(void){return (int)sizeof(vx_completion) - 32;}\n')
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-c", str(c),
+                    "-o", str(tmp_path / "t.o")], check=True)
+
+
+def test_completion_layout():
+    from vortex_amd._lib import vx_completion, vx_config
+
+    assert ctypes.sizeof(vx_completion) == 32
+    assert vx_completion.digest.offset == 9
+    assert ctypes.sizeof(vx_config) == 24
+
+
+def test_library_exports_declared_symbols(built):
+    from vortex_amd import _lib
+
+    lib = _lib.lib()
+    decl = declared_symbols()
+    assert decl == set(_lib.EXPORTS)
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (vx_[a-z0-9_]+)", out))
+    missing = decl - exported
+    assert not missing, missing
+    for name in decl:
+        assert hasattr(lib, name)
+    assert lib.vx_abi_version() == 1
+
+
+def test_no_cpu_fallback_in_product():
+    """The product path never imports or links the oracle."""
+    for dirpath, _, files in os.walk(os.path.join(ROOT, "vortex_amd")):
+        for f in files:
+            if f.endswith((".py", ".hip", ".hpp", ".h", ".cpp")):
+                code = [ln for ln in open(os.path.join(dirpath, f)).read().splitlines()
+                        if not ln.lstrip().startswith(("//", "#", "*", "/*"))]
+                text = "\n".join(code)
+                assert "import oracle" not in text and "from oracle" not in text, f
+                assert "liboracle" not in text and not re.search(r"\bvxo_\w+\s*\(", text), f
+
+
+def test_validation_without_gpu(built):
+    from vortex_amd import _lib
+
+    L = _lib.lib()
+    # argument errors are reported before anything touches a device
+    assert L.vx_sha1_device_uniform(None, 64, 64, 4, None, None, None, None) == _lib.VX_EINVAL
+    assert L.vx_sha1_device_uniform(ctypes.c_void_p(0x1001), 64, 64, 4, ctypes.c_void_p(0x2000), None, None,
+                                    None) == _lib.VX_EINVAL  # misaligned base
+    assert L.vx_sha1_device_uniform(ctypes.c_void_p(0x1000), 24, 64, 4, ctypes.c_void_p(0x2000), None, None,
+                                    None) == _lib.VX_EINVAL  # stride % 16
+    assert L.vx_sha1_device_uniform(ctypes.c_void_p(0x1000), 64, 64, 0, None, None, None, None) == 0  # n=0 no-op
+    assert b"aligned" in L.vx_last_error() or L.vx_last_error()
+    assert L.vx_strerror(_lib.VX_ERANGE) == b"piece longer than max_piece_len"
+    cfg = _lib.vx_config()
+    L.vx_config_default(ctypes.byref(cfg), 262144)
+    assert cfg.max_piece_len == 262144 and cfg.slots >= 1 and cfg.batch_pieces >= 1
+    assert cfg.slot_bytes >= 262144
+    h = ctypes.c_void_p()
+    if L.vx_device_count() == 0:
+        assert L.vx_create(ctypes.byref(cfg), ctypes.byref(h)) == _lib.VX_ENODEV
+    bad = _lib.vx_config()
+    assert L.vx_create(ctypes.byref(bad), ctypes.byref(h)) == _lib.VX_EINVAL
+    assert L.vx_create(None, ctypes.byref(h)) == _lib.VX_EINVAL
+
+
+def test_sort_order_host_helper(built):
+    import numpy as np
+
+    from vortex_amd import _lib
+
+    lens = np.array([5, 100, 7, 100, 0, 64], dtype=np.uint32)
+    out = np.zeros_like(lens)
+    assert _lib.lib().vx_sort_order(lens.ctypes.data, lens.size, out.ctypes.data) == 0
+    assert out.tolist() == [1, 3, 5, 2, 0, 4]  # descending, stable
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    from vortex_amd import _lib
+
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(ImportError):
+        _lib.lib()

@@ -1,0 +1,117 @@
+"""ctypes binding of libvortex_amd.so (the C ABI declared in include/vx_hash.h).
+
+The library is the product: there is no CPU or PyTorch fallback.  If it is
+missing, loading raises ``ImportError`` (fail loudly, never silently degrade).
+
+``torch`` is imported before the library is loaded on purpose: torch ships its
+own ``libamdhip64.so`` (same soname ``libamdhip64.so.7``) and loading it first
+makes our library bind to that single HIP runtime instead of pulling in a
+second one from /opt/rocm.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libvortex_amd.so")
+
+VX_OK = 0
+VX_EINVAL = -22
+VX_ENOMEM = -12
+VX_ERANGE = -34
+VX_ENODEV = -19
+VX_EDEVICE = -5
+VX_EBUSY = -16
+
+# Every symbol include/vx_hash.h and include/vx_synth.h declare (checked by
+# tests/test_abi.py against the headers and the library's dynamic symbols).
+EXPORTS = (
+    "vx_abi_version", "vx_last_error", "vx_strerror", "vx_device_count", "vx_config_default",
+    "vx_create", "vx_destroy", "vx_register_host_buffer", "vx_unregister_host_buffer",
+    "vx_submit", "vx_flush", "vx_poll", "vx_drain", "vx_pending",
+    "vx_sha1_batch", "vx_verify_batch",
+    "vx_sha1_device_uniform", "vx_sha1_device_ragged", "vx_sort_order",
+    "vx_synth_fill",
+)
+
+
+class VxError(RuntimeError):
+    def __init__(self, code: int, where: str, msg: str):
+        super().__init__(f"{where} failed: {code} ({msg})")
+        self.code = code
+
+
+class vx_completion(ctypes.Structure):
+    _fields_ = [("tag", ctypes.c_uint64), ("matched", ctypes.c_uint8), ("digest", ctypes.c_uint8 * 20),
+                ("_pad", ctypes.c_uint8 * 3)]
+
+
+class vx_config(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int32), ("max_piece_len", ctypes.c_uint32), ("batch_pieces", ctypes.c_uint32),
+                ("slots", ctypes.c_uint32), ("slot_bytes", ctypes.c_uint64)]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def _declare(L: ctypes.CDLL) -> None:
+    c = ctypes
+    vp = c.c_void_p
+    sig = {
+        "vx_abi_version": ([], c.c_int),
+        "vx_last_error": ([], c.c_char_p),
+        "vx_strerror": ([c.c_int], c.c_char_p),
+        "vx_device_count": ([], c.c_int),
+        "vx_config_default": ([c.POINTER(vx_config), c.c_uint32], None),
+        "vx_create": ([c.POINTER(vx_config), c.POINTER(vp)], c.c_int),
+        "vx_destroy": ([vp], c.c_int),
+        "vx_register_host_buffer": ([vp, vp, c.c_size_t], c.c_int),
+        "vx_unregister_host_buffer": ([vp, vp], c.c_int),
+        "vx_submit": ([vp, c.c_uint64, vp, c.c_uint32, vp], c.c_int),
+        "vx_flush": ([vp], c.c_int),
+        "vx_poll": ([vp, c.POINTER(vx_completion), c.c_size_t], c.c_int64),
+        "vx_drain": ([vp, c.c_uint32], c.c_int),
+        "vx_pending": ([vp], c.c_uint64),
+        "vx_sha1_batch": ([vp, vp, vp, c.c_size_t, vp], c.c_int),
+        "vx_verify_batch": ([vp, vp, vp, vp, c.c_size_t, vp, vp], c.c_int),
+        "vx_sha1_device_uniform": ([vp, c.c_uint64, c.c_uint32, c.c_uint32, vp, vp, vp, vp], c.c_int),
+        "vx_sha1_device_ragged": ([vp, vp, vp, vp, c.c_uint32, vp, vp, vp, vp], c.c_int),
+        "vx_sort_order": ([vp, c.c_uint32, vp], c.c_int),
+        "vx_synth_fill": ([vp, c.c_uint64, c.c_uint32, c.c_uint32, c.c_uint64, c.c_uint64, c.c_uint32, vp],
+                          c.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+
+
+def lib() -> ctypes.CDLL:
+    """Load libvortex_amd.so once; raise ImportError if it was never built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            import torch  # noqa: F401  (single HIP runtime, see module doc)
+
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"{LIB_PATH} is missing: the HIP engine is not built. Run "
+                    "`python -c 'import __graft_entry__ as g; g.build()'` (or `make -C vortex_amd/csrc`).")
+            L = ctypes.CDLL(LIB_PATH)
+            _declare(L)
+            if L.vx_abi_version() != 1:
+                raise ImportError("libvortex_amd.so ABI version mismatch")
+            _lib = L
+    return _lib
+
+
+def check(rc: int, where: str) -> int:
+    if rc < 0:
+        msg = lib().vx_last_error().decode(errors="replace")
+        raise VxError(rc, where, msg)
+    return rc

@@ -1,0 +1,559 @@
+// vx_engine.hip — host side of the C ABI in include/vx_hash.h.
+//
+// Replaces, on the host, what vortex does around its hashing pool:
+//  * vx_submit / vx_flush / vx_poll: the scope.spawn → mpsc → try_recv cycle
+//    (peer_connection.rs:1145-1158 → torrent.rs:415-442), batched for the GPU.
+//  * vx_sha1_batch / vx_verify_batch: the par_iter bulk verify
+//    (torrent.rs:724-740).
+//  * vx_sha1_device_*: enqueue the kernels on device-resident batches.
+//
+// Design (DESIGN.md "Host engine"): a context owns `slots` batch slots, each
+// with its own HIP stream, a device arena, a pinned staging arena and pinned
+// metadata.  Pieces are appended to the filling slot at 256-byte aligned
+// offsets: pieces inside a registered (pinned) host range are DMA'd straight
+// from the caller's buffer at submit time; others are memcpy'd into the
+// slot's pinned stage and moved with one H2D per contiguous run at launch.
+// A launch is H2D(meta) → kernel → D2H(digests, verdicts) → event; slots on
+// different streams overlap copy and compute.  vx_poll harvests finished
+// slots without blocking.  No internal threads: like the reference's loop,
+// everything is driven from the caller's thread.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <numeric>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "vx_hash.h"
+#include "vx_kernels.h"
+#include "vx_synth.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    g_err = std::string(what) + ": " + hipGetErrorString(e);
+    return VX_EDEVICE;
+}
+
+#define VX_HIP(call)                                      \
+    do {                                                  \
+        hipError_t _e = (call);                           \
+        if (_e != hipSuccess) return hip_fail(_e, #call); \
+    } while (0)
+
+constexpr uint64_t kAlign = 256;
+
+uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+struct Run {
+    uint64_t lo, hi;  // staged byte range [lo, hi) of the arena
+};
+
+struct Slot {
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    uint64_t arena_cap = 0;
+    uint32_t cap = 0;  // pieces
+    uint8_t* d_arena = nullptr;
+    uint8_t* h_stage = nullptr;
+    // pinned metadata block: offsets | lens | expected | digests | matched
+    uint8_t* h_meta = nullptr;
+    uint8_t* d_meta = nullptr;
+    uint64_t* h_offsets = nullptr;
+    uint32_t* h_lens = nullptr;
+    uint8_t* h_expected = nullptr;
+    uint8_t* h_digests = nullptr;
+    uint8_t* h_matched = nullptr;
+    uint64_t* d_offsets = nullptr;
+    uint32_t* d_lens = nullptr;
+    uint8_t* d_expected = nullptr;
+    uint8_t* d_digests = nullptr;
+    uint8_t* d_matched = nullptr;
+    std::vector<uint64_t> tags;
+    std::vector<Run> runs;
+    uint32_t n = 0;
+    uint64_t bytes = 0;
+    bool uniform = true;
+    bool has_expected = false;
+    enum State { FREE, FILLING, INFLIGHT } state = FREE;
+    uint64_t seq = 0;
+};
+
+}  // namespace
+
+struct vx_ctx {
+    vx_config cfg{};
+    std::vector<Slot> slots;
+    int filling = -1;
+    std::deque<vx_completion> done;
+    std::map<uintptr_t, size_t> registered;
+    uint64_t pending = 0;
+    uint64_t seq = 0;
+    int sticky = 0;
+};
+
+namespace {
+
+int set_device(const vx_ctx* c) {
+    VX_HIP(hipSetDevice(c->cfg.device));
+    return 0;
+}
+
+bool is_registered(const vx_ctx* c, const void* p, size_t len) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    auto it = c->registered.upper_bound(a);
+    if (it == c->registered.begin()) return false;
+    --it;
+    return a >= it->first && a + len <= it->first + it->second;
+}
+
+int free_slot_mem(Slot& s) {
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.done) (void)hipEventDestroy(s.done);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    if (s.d_arena) (void)hipFree(s.d_arena);
+    if (s.d_meta) (void)hipFree(s.d_meta);
+    if (s.h_stage) (void)hipHostFree(s.h_stage);
+    if (s.h_meta) (void)hipHostFree(s.h_meta);
+    s = Slot{};
+    return 0;
+}
+
+int alloc_slot(Slot& s, uint64_t arena, uint32_t cap) {
+    s.arena_cap = arena;
+    s.cap = cap;
+    VX_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    VX_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    if (hipMalloc(&s.d_arena, arena) != hipSuccess) return fail(VX_ENOMEM, "device arena allocation failed");
+    if (hipHostMalloc(&s.h_stage, arena, hipHostMallocDefault) != hipSuccess)
+        return fail(VX_ENOMEM, "pinned stage allocation failed");
+    const size_t meta = (size_t)cap * (8 + 4 + 20 + 20 + 1) + 64;
+    if (hipHostMalloc(&s.h_meta, meta, hipHostMallocDefault) != hipSuccess)
+        return fail(VX_ENOMEM, "pinned metadata allocation failed");
+    if (hipMalloc(&s.d_meta, meta) != hipSuccess) return fail(VX_ENOMEM, "device metadata allocation failed");
+    auto carve = [cap](uint8_t* b, uint64_t*& off, uint32_t*& lens, uint8_t*& exp, uint8_t*& dig, uint8_t*& m) {
+        off = reinterpret_cast<uint64_t*>(b);
+        lens = reinterpret_cast<uint32_t*>(b + (size_t)cap * 8);
+        exp = b + (size_t)cap * 12;
+        dig = b + (size_t)cap * 32;
+        m = b + (size_t)cap * 52;
+    };
+    carve(s.h_meta, s.h_offsets, s.h_lens, s.h_expected, s.h_digests, s.h_matched);
+    carve(s.d_meta, s.d_offsets, s.d_lens, s.d_expected, s.d_digests, s.d_matched);
+    s.tags.reserve(cap);
+    return 0;
+}
+
+void reset_fill(Slot& s) {
+    s.tags.clear();
+    s.runs.clear();
+    s.n = 0;
+    s.bytes = 0;
+    s.uniform = true;
+    s.has_expected = false;
+}
+
+int launch_slot(vx_ctx* c, int si) {
+    Slot& s = c->slots[si];
+    if (c->filling == si) c->filling = -1;
+    if (s.n == 0) {
+        s.state = Slot::FREE;
+        return 0;
+    }
+    for (const Run& r : s.runs)
+        VX_HIP(hipMemcpyAsync(s.d_arena + r.lo, s.h_stage + r.lo, r.hi - r.lo, hipMemcpyHostToDevice, s.stream));
+    const uint32_t n = s.n;
+    if (s.has_expected)
+        VX_HIP(hipMemcpyAsync(s.d_expected, s.h_expected, (size_t)n * 20, hipMemcpyHostToDevice, s.stream));
+    hipError_t e;
+    if (s.uniform) {
+        const uint32_t len = s.h_lens[0];
+        const uint64_t stride = align_up(std::max<uint32_t>(len, 1), kAlign);
+        e = vx::launch_uniform(s.d_arena, stride, len, n, s.d_digests, s.has_expected ? s.d_expected : nullptr,
+                               s.d_matched, s.stream);
+    } else {
+        VX_HIP(hipMemcpyAsync(s.d_offsets, s.h_offsets, (size_t)n * 8, hipMemcpyHostToDevice, s.stream));
+        VX_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)n * 4, hipMemcpyHostToDevice, s.stream));
+        e = vx::launch_ragged(s.d_arena, s.d_offsets, s.d_lens, nullptr, n, s.d_digests,
+                              s.has_expected ? s.d_expected : nullptr, s.d_matched, s.stream);
+    }
+    if (e != hipSuccess) return hip_fail(e, "kernel launch");
+    VX_HIP(hipMemcpyAsync(s.h_digests, s.d_digests, (size_t)n * 20, hipMemcpyDeviceToHost, s.stream));
+    if (s.has_expected)
+        VX_HIP(hipMemcpyAsync(s.h_matched, s.d_matched, n, hipMemcpyDeviceToHost, s.stream));
+    VX_HIP(hipEventRecord(s.done, s.stream));
+    s.state = Slot::INFLIGHT;
+    s.seq = c->seq++;
+    return 0;
+}
+
+void harvest(vx_ctx* c, Slot& s) {
+    for (uint32_t i = 0; i < s.n; ++i) {
+        vx_completion r{};
+        r.tag = s.tags[i];
+        r.matched = s.has_expected ? s.h_matched[i] : 0;
+        std::memcpy(r.digest, s.h_digests + (size_t)i * 20, 20);
+        c->done.push_back(r);
+    }
+    reset_fill(s);
+    s.state = Slot::FREE;
+}
+
+// Harvest finished slots (oldest first).  block=true waits for the oldest.
+int reap(vx_ctx* c, bool block_oldest) {
+    std::vector<int> order;
+    for (int i = 0; i < (int)c->slots.size(); ++i)
+        if (c->slots[i].state == Slot::INFLIGHT) order.push_back(i);
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return c->slots[a].seq < c->slots[b].seq; });
+    bool first = true;
+    for (int i : order) {
+        Slot& s = c->slots[i];
+        hipError_t q = (block_oldest && first) ? hipEventSynchronize(s.done) : hipEventQuery(s.done);
+        first = false;
+        if (q == hipSuccess) {
+            harvest(c, s);
+        } else if (q != hipErrorNotReady) {
+            c->sticky = hip_fail(q, "batch failed on device");
+            return c->sticky;
+        }
+    }
+    return 0;
+}
+
+int acquire_filling(vx_ctx* c) {
+    if (c->filling >= 0) return c->filling;
+    for (;;) {
+        for (int i = 0; i < (int)c->slots.size(); ++i) {
+            if (c->slots[i].state == Slot::FREE) {
+                reset_fill(c->slots[i]);
+                c->slots[i].state = Slot::FILLING;
+                c->filling = i;
+                return i;
+            }
+        }
+        int rc = reap(c, /*block_oldest=*/true);
+        if (rc) return rc;
+    }
+}
+
+int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, const uint8_t* expected) {
+    if (c->sticky) return c->sticky;
+    if (!data && len) return fail(VX_EINVAL, "vx_submit: data is NULL");
+    if (len > c->cfg.max_piece_len) return fail(VX_ERANGE, "vx_submit: piece longer than max_piece_len");
+    int si = acquire_filling(c);
+    if (si < 0) return si;
+    Slot* s = &c->slots[si];
+    uint64_t off = align_up(s->bytes, kAlign);
+    if (s->n == s->cap || off + len > s->arena_cap) {
+        int rc = launch_slot(c, si);
+        if (rc) return rc;
+        si = acquire_filling(c);
+        if (si < 0) return si;
+        s = &c->slots[si];
+        off = 0;
+    }
+    const uint32_t i = s->n;
+    if (len) {
+        if (is_registered(c, data, len)) {
+            VX_HIP(hipMemcpyAsync(s->d_arena + off, data, len, hipMemcpyHostToDevice, s->stream));
+        } else {
+            std::memcpy(s->h_stage + off, data, len);
+            if (!s->runs.empty() && s->runs.back().hi == off)
+                s->runs.back().hi = off + len;
+            else if (!s->runs.empty() && align_up(s->runs.back().hi, kAlign) == off)
+                s->runs.back().hi = off + len;  // alignment gap travels too
+            else
+                s->runs.push_back(Run{off, off + len});
+        }
+    }
+    s->h_offsets[i] = off;
+    s->h_lens[i] = len;
+    // Equal lengths at 256-byte aligned back-to-back offsets are a uniform
+    // batch: offset(i) = i * align_up(len, 256) (the uniform kernel's layout).
+    if (i > 0 && len != s->h_lens[0]) s->uniform = false;
+    if (expected) {
+        std::memcpy(s->h_expected + (size_t)i * 20, expected, 20);
+        if (i > 0 && !s->has_expected) {
+            // earlier pieces of this batch had no expected digest: they get
+            // matched = 0 against a zero table, which nobody reads.
+            std::memset(s->h_expected, 0, (size_t)i * 20);
+        }
+        s->has_expected = true;
+    } else if (s->has_expected) {
+        std::memset(s->h_expected + (size_t)i * 20, 0, 20);
+    }
+    s->tags.push_back(tag);
+    s->n = i + 1;
+    s->bytes = off + std::max<uint32_t>(len, 1);
+    c->pending++;
+    if (s->n >= c->cfg.batch_pieces) return launch_slot(c, si);
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int vx_abi_version(void) { return VX_ABI_VERSION; }
+
+const char* vx_last_error(void) { return g_err.c_str(); }
+
+const char* vx_strerror(int code) {
+    switch (code) {
+        case VX_OK: return "ok";
+        case VX_EINVAL: return "invalid argument";
+        case VX_ENOMEM: return "out of memory";
+        case VX_ERANGE: return "piece longer than max_piece_len";
+        case VX_ENODEV: return "no such device";
+        case VX_EDEVICE: return "HIP runtime error";
+        case VX_EBUSY: return "busy: work in flight";
+        default: return "unknown error";
+    }
+}
+
+int vx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void vx_config_default(vx_config* cfg, uint32_t max_piece_len) {
+    if (!cfg) return;
+    cfg->device = 0;
+    cfg->max_piece_len = max_piece_len;
+    cfg->slots = 4;
+    cfg->slot_bytes = std::max<uint64_t>(128ull << 20, align_up(max_piece_len, kAlign) * 16);
+    cfg->batch_pieces = (uint32_t)std::min<uint64_t>(65536, cfg->slot_bytes / align_up(std::max<uint32_t>(max_piece_len, 1), kAlign));
+}
+
+int vx_create(const vx_config* cfg, vx_ctx** out) {
+    if (!cfg || !out) return fail(VX_EINVAL, "vx_create: NULL argument");
+    *out = nullptr;
+    if (cfg->max_piece_len == 0 || cfg->slots == 0 || cfg->batch_pieces == 0)
+        return fail(VX_EINVAL, "vx_create: max_piece_len, slots and batch_pieces must be > 0");
+    if (cfg->slot_bytes < cfg->max_piece_len) return fail(VX_EINVAL, "vx_create: slot_bytes < max_piece_len");
+    const int ndev = vx_device_count();
+    if (cfg->device < 0 || cfg->device >= ndev) return fail(VX_ENODEV, "vx_create: no such HIP device");
+    vx_ctx* c = new (std::nothrow) vx_ctx();
+    if (!c) return fail(VX_ENOMEM, "vx_create: out of host memory");
+    c->cfg = *cfg;
+    int rc = set_device(c);
+    if (!rc) {
+        c->slots.resize(cfg->slots);
+        for (auto& s : c->slots) {
+            rc = alloc_slot(s, cfg->slot_bytes, cfg->batch_pieces);
+            if (rc) break;
+        }
+    }
+    if (rc) {
+        for (auto& s : c->slots) free_slot_mem(s);
+        delete c;
+        return rc;
+    }
+    *out = c;
+    return 0;
+}
+
+int vx_destroy(vx_ctx* c) {
+    if (!c) return 0;
+    int rc = c->sticky ? 0 : vx_drain(c, 0);
+    set_device(c);
+    for (auto& r : c->registered) (void)hipHostUnregister(reinterpret_cast<void*>(r.first));
+    for (auto& s : c->slots) free_slot_mem(s);
+    delete c;
+    return rc;
+}
+
+int vx_register_host_buffer(vx_ctx* c, void* ptr, size_t len) {
+    if (!c || !ptr || !len) return fail(VX_EINVAL, "vx_register_host_buffer: bad argument");
+    const uintptr_t a = reinterpret_cast<uintptr_t>(ptr);
+    auto it = c->registered.lower_bound(a);
+    if (it != c->registered.end() && it->first < a + len) return fail(VX_EINVAL, "overlapping registration");
+    if (it != c->registered.begin()) {
+        auto p = std::prev(it);
+        if (p->first + p->second > a) return fail(VX_EINVAL, "overlapping registration");
+    }
+    int rc = set_device(c);
+    if (rc) return rc;
+    VX_HIP(hipHostRegister(ptr, len, hipHostRegisterDefault));
+    c->registered[a] = len;
+    return 0;
+}
+
+int vx_unregister_host_buffer(vx_ctx* c, void* ptr) {
+    if (!c || !ptr) return fail(VX_EINVAL, "vx_unregister_host_buffer: bad argument");
+    auto it = c->registered.find(reinterpret_cast<uintptr_t>(ptr));
+    if (it == c->registered.end()) return fail(VX_EINVAL, "pointer was not registered");
+    if (c->pending) return fail(VX_EBUSY, "unregister with pieces in flight");
+    int rc = set_device(c);
+    if (rc) return rc;
+    VX_HIP(hipHostUnregister(ptr));
+    c->registered.erase(it);
+    return 0;
+}
+
+int vx_submit(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, const uint8_t* expected) {
+    if (!c) return fail(VX_EINVAL, "vx_submit: NULL context");
+    int rc = set_device(c);
+    if (rc) return rc;
+    return submit_impl(c, tag, data, len, expected);
+}
+
+int vx_flush(vx_ctx* c) {
+    if (!c) return fail(VX_EINVAL, "vx_flush: NULL context");
+    if (c->sticky) return c->sticky;
+    if (c->filling < 0) return 0;
+    int rc = set_device(c);
+    if (rc) return rc;
+    return launch_slot(c, c->filling);
+}
+
+int64_t vx_poll(vx_ctx* c, vx_completion* out, size_t max) {
+    if (!c || (!out && max)) return fail(VX_EINVAL, "vx_poll: bad argument");
+    if (c->sticky) return c->sticky;
+    int rc = set_device(c);
+    if (rc) return rc;
+    rc = reap(c, false);
+    if (rc) return rc;
+    size_t k = 0;
+    while (k < max && !c->done.empty()) {
+        out[k++] = c->done.front();
+        c->done.pop_front();
+    }
+    c->pending -= k;
+    return (int64_t)k;
+}
+
+int vx_drain(vx_ctx* c, uint32_t timeout_ms) {
+    if (!c) return fail(VX_EINVAL, "vx_drain: NULL context");
+    int rc = vx_flush(c);
+    if (rc) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        bool any = false;
+        for (auto& s : c->slots) any |= s.state == Slot::INFLIGHT;
+        if (!any) return 0;
+        if (timeout_ms == 0) {
+            rc = reap(c, true);
+        } else {
+            rc = reap(c, false);
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(timeout_ms))
+                return fail(VX_EBUSY, "vx_drain: timeout");
+            std::this_thread::sleep_for(std::chrono::microseconds(100));
+        }
+        if (rc) return rc;
+    }
+}
+
+uint64_t vx_pending(const vx_ctx* c) { return c ? c->pending : 0; }
+
+static int batch_impl(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, const uint8_t* expected, size_t n,
+                      uint8_t* matched_out, uint8_t* digests_out) {
+    if (!c) return fail(VX_EINVAL, "batch: NULL context");
+    if (n && (!ptrs || !lens)) return fail(VX_EINVAL, "batch: NULL ptrs/lens");
+    if (c->pending) return fail(VX_EBUSY, "batch: async pieces pending; drain and poll first");
+    int rc = set_device(c);
+    if (rc) return rc;
+    std::vector<vx_completion> buf(1024);
+    size_t got = 0;
+    auto collect = [&]() -> int {
+        for (;;) {
+            int64_t k = vx_poll(c, buf.data(), buf.size());
+            if (k < 0) return (int)k;
+            for (int64_t j = 0; j < k; ++j) {
+                const vx_completion& r = buf[j];
+                if (digests_out) std::memcpy(digests_out + r.tag * 20, r.digest, 20);
+                if (matched_out) matched_out[r.tag] = r.matched;
+            }
+            got += (size_t)k;
+            if ((size_t)k < buf.size()) return 0;
+        }
+    };
+    for (size_t i = 0; i < n; ++i) {
+        rc = submit_impl(c, i, ptrs[i], lens[i], expected ? expected + i * 20 : nullptr);
+        if (rc) return rc;
+        if ((i & 255) == 255 && (rc = collect())) return rc;
+    }
+    if ((rc = vx_drain(c, 0))) return rc;
+    if ((rc = collect())) return rc;
+    if (got != n) return fail(VX_EDEVICE, "batch: lost completions");
+    return 0;
+}
+
+int vx_sha1_batch(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, size_t n, uint8_t* digests_out) {
+    if (!digests_out && n) return fail(VX_EINVAL, "vx_sha1_batch: NULL digests_out");
+    return batch_impl(c, ptrs, lens, nullptr, n, nullptr, digests_out);
+}
+
+int vx_verify_batch(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, const uint8_t* expected, size_t n,
+                    uint8_t* matched_out, uint8_t* digests_out) {
+    if (n && (!expected || !matched_out)) return fail(VX_EINVAL, "vx_verify_batch: NULL expected/matched_out");
+    return batch_impl(c, ptrs, lens, expected, n, matched_out, digests_out);
+}
+
+int vx_sha1_device_uniform(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
+                           const void* d_expected, void* d_matched, void* stream) {
+    if (n == 0) return 0;
+    if (!d_base) return fail(VX_EINVAL, "vx_sha1_device_uniform: NULL base");
+    if (!d_digests && !(d_expected && d_matched))
+        return fail(VX_EINVAL, "vx_sha1_device_uniform: need d_digests or d_expected+d_matched");
+    if (d_matched && !d_expected) return fail(VX_EINVAL, "vx_sha1_device_uniform: d_matched needs d_expected");
+    if ((reinterpret_cast<uintptr_t>(d_base) & 15) || (stride & 15))
+        return fail(VX_EINVAL, "vx_sha1_device_uniform: base and stride must be 16-byte aligned");
+    if (n > 1 && stride < len) return fail(VX_EINVAL, "vx_sha1_device_uniform: stride < len");
+    hipError_t e = vx::launch_uniform(static_cast<const uint8_t*>(d_base), stride, len, n,
+                                      static_cast<uint8_t*>(d_digests), static_cast<const uint8_t*>(d_expected),
+                                      static_cast<uint8_t*>(d_matched), static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "sha1_uniform_kernel launch");
+    return 0;
+}
+
+int vx_sha1_device_ragged(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
+                          const uint32_t* d_order, uint32_t n, void* d_digests, const void* d_expected,
+                          void* d_matched, void* stream) {
+    if (n == 0) return 0;
+    if (!d_base || !d_offsets || !d_lens) return fail(VX_EINVAL, "vx_sha1_device_ragged: NULL argument");
+    if (!d_digests && !(d_expected && d_matched))
+        return fail(VX_EINVAL, "vx_sha1_device_ragged: need d_digests or d_expected+d_matched");
+    if (d_matched && !d_expected) return fail(VX_EINVAL, "vx_sha1_device_ragged: d_matched needs d_expected");
+    if (reinterpret_cast<uintptr_t>(d_base) & 15)
+        return fail(VX_EINVAL, "vx_sha1_device_ragged: base must be 16-byte aligned");
+    hipError_t e = vx::launch_ragged(static_cast<const uint8_t*>(d_base), d_offsets, d_lens, d_order, n,
+                                     static_cast<uint8_t*>(d_digests), static_cast<const uint8_t*>(d_expected),
+                                     static_cast<uint8_t*>(d_matched), static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "sha1_ragged_kernel launch");
+    return 0;
+}
+
+int vx_sort_order(const uint32_t* lens, uint32_t n, uint32_t* order_out) {
+    if (n && (!lens || !order_out)) return fail(VX_EINVAL, "vx_sort_order: NULL argument");
+    std::iota(order_out, order_out + n, 0u);
+    std::stable_sort(order_out, order_out + n, [lens](uint32_t a, uint32_t b) { return lens[a] > lens[b]; });
+    return 0;
+}
+
+int vx_synth_fill(void* d_base, uint64_t stride, uint32_t len, uint32_t n, uint64_t first, uint64_t seed,
+                  uint32_t corrupt_every, void* stream) {
+    if (n == 0) return 0;
+    if (!d_base) return fail(VX_EINVAL, "vx_synth_fill: NULL base");
+    if ((reinterpret_cast<uintptr_t>(d_base) & 15) || (stride & 15) || (n > 1 && stride < len))
+        return fail(VX_EINVAL, "vx_synth_fill: base/stride must be 16-byte aligned and stride >= len");
+    hipError_t e = vx::launch_synth_fill(static_cast<uint8_t*>(d_base), stride, len, n, first, seed, corrupt_every,
+                                         static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return hip_fail(e, "synth launch");
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,228 @@
+"""Host-side mirror of vortex's hashing-pool boundary, backed by the HIP engine.
+
+The reference has no trait for this path; its "interface" is three call sites
+(SURVEY.md §8b), mirrored here under the reference's own names:
+
+===============================  ==============================================
+reference                        here
+===============================  ==============================================
+``scope.spawn(hash closure)``    :meth:`HashPool.spawn`
+  peer_connection.rs:1139-1158     (index, conn_id, buffer, piece_len, expected)
+``downloaded_piece_rc.try_recv`` :meth:`HashPool.try_recv` → ``DownloadedPiece``
+  torrent.rs:415-442
+``DownloadedPiece``              :class:`DownloadedPiece` (piece_selector.rs:311-317)
+``par_iter().map(check).collect``:func:`verify_pieces` → ``list[bool]``
+  torrent.rs:724-740
+===============================  ==============================================
+
+Semantics kept from the reference:
+* a hash mismatch is a value (``hash_matched=False``), never an exception;
+* the buffer is moved into the job and handed back in ``DownloadedPiece``
+  (the caller must return it to its pool, buf_pool.rs:21-30);
+* the digest covers exactly ``buffer[:piece_len]`` (peer_connection.rs:1148) —
+  pool buffers are reused without zeroing, bytes past piece_len are ignored;
+* completions arrive in batch-completion order, not submission order.
+
+All hashing runs in libvortex_amd.so on the GPU; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Any, Iterable, Optional, Sequence
+
+from . import _lib
+from ._lib import check, lib, vx_completion, vx_config
+
+
+@dataclass
+class DownloadedPiece:
+    """piece_selector.rs:311-317."""
+
+    index: int
+    conn_id: int
+    hash_matched: bool
+    buffer: Any
+    digest: bytes = b""
+
+
+def _addr_of(buf) -> tuple[int, Any]:
+    """Stable address of a writable or read-only buffer plus a keep-alive."""
+    if isinstance(buf, (bytes,)):
+        keep = ctypes.create_string_buffer(buf, len(buf))
+        return ctypes.addressof(keep), keep
+    try:
+        import numpy as np
+
+        if isinstance(buf, np.ndarray):
+            return buf.ctypes.data, buf
+    except ImportError:  # pragma: no cover
+        pass
+    mv = memoryview(buf)
+    if mv.readonly:
+        keep = ctypes.create_string_buffer(mv.tobytes(), mv.nbytes)
+        return ctypes.addressof(keep), keep
+    c = (ctypes.c_uint8 * mv.nbytes).from_buffer(mv)
+    return ctypes.addressof(c), (c, mv)
+
+
+class HashPool:
+    """The GPU engine behind vortex's spawn / try_recv hash boundary.
+
+    ``piece_length`` is the torrent's piece_length (the BufferPool buffer
+    size, torrent.rs:344).  One HashPool per torrent, used from one thread.
+    """
+
+    def __init__(self, piece_length: int, device: int = 0, slots: Optional[int] = None,
+                 batch_pieces: Optional[int] = None, slot_bytes: Optional[int] = None):
+        L = lib()
+        cfg = vx_config()
+        L.vx_config_default(ctypes.byref(cfg), piece_length)
+        cfg.device = device
+        if slots is not None:
+            cfg.slots = slots
+        if slot_bytes is not None:
+            cfg.slot_bytes = slot_bytes
+        if batch_pieces is not None:
+            cfg.batch_pieces = batch_pieces
+        h = ctypes.c_void_p()
+        check(L.vx_create(ctypes.byref(cfg), ctypes.byref(h)), "vx_create")
+        self._h = h
+        self.config = cfg
+        self._next_tag = 0
+        self._inflight: dict[int, tuple[int, int, Any, Any]] = {}
+        self._cbuf = (vx_completion * 1024)()
+        self._registered: dict[int, Any] = {}
+
+    # -- lifecycle ---------------------------------------------------------
+    def close(self) -> None:
+        if self._h:
+            check(lib().vx_destroy(self._h), "vx_destroy")
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- buffer pinning (buf_pool.rs / buf_ring.rs AnonymousMmap) -----------
+    def register_buffer(self, buf) -> None:
+        addr, keep = _addr_of(buf)
+        n = memoryview(buf).nbytes
+        check(lib().vx_register_host_buffer(self._h, addr, n), "vx_register_host_buffer")
+        self._registered[addr] = keep
+
+    def unregister_buffer(self, buf) -> None:
+        addr, _ = _addr_of(buf)
+        check(lib().vx_unregister_host_buffer(self._h, addr), "vx_unregister_host_buffer")
+        self._registered.pop(addr, None)
+
+    # -- download path -------------------------------------------------------
+    def spawn(self, index: int, conn_id: int, buffer, piece_len: int, expected_hash: bytes) -> None:
+        """peer_connection.rs:1145-1158: hash buffer[:piece_len] against
+        expected_hash; the result comes back from try_recv()."""
+        if len(expected_hash) != 20:
+            raise ValueError("expected_hash must be 20 bytes")
+        addr, keep = _addr_of(buffer)
+        if piece_len > memoryview(buffer).nbytes:
+            raise ValueError("piece_len exceeds buffer size")
+        tag = self._next_tag
+        self._next_tag += 1
+        exp = ctypes.create_string_buffer(bytes(expected_hash), 20)
+        check(lib().vx_submit(self._h, tag, addr, piece_len, exp), "vx_submit")
+        self._inflight[tag] = (index, conn_id, buffer, keep)
+
+    def flush(self) -> None:
+        """Launch everything queued; call once per event-loop turn."""
+        check(lib().vx_flush(self._h), "vx_flush")
+
+    def _poll(self, max_items: int) -> list[DownloadedPiece]:
+        k = check(lib().vx_poll(self._h, self._cbuf, min(max_items, len(self._cbuf))), "vx_poll")
+        out = []
+        for j in range(k):
+            r = self._cbuf[j]
+            index, conn_id, buffer, _keep = self._inflight.pop(r.tag)
+            out.append(DownloadedPiece(index, conn_id, bool(r.matched), buffer, bytes(r.digest)))
+        return out
+
+    def try_recv(self) -> Optional[DownloadedPiece]:
+        """torrent.rs:418 `downloaded_piece_rc.try_recv()`: non-blocking."""
+        got = self._poll(1)
+        return got[0] if got else None
+
+    def try_iter(self) -> list[DownloadedPiece]:
+        """Everything completed so far (the `while let Ok(..) = try_recv()` loop)."""
+        out = []
+        while True:
+            got = self._poll(len(self._cbuf))
+            out.extend(got)
+            if len(got) < len(self._cbuf):
+                return out
+
+    def drain(self, timeout_ms: int = 0) -> None:
+        """Flush and wait for all in-flight pieces (the scope join of
+        event_loop.rs:385-602); results stay queued for try_recv."""
+        check(lib().vx_drain(self._h, timeout_ms), "vx_drain")
+
+    @property
+    def pending(self) -> int:
+        return int(lib().vx_pending(self._h))
+
+    # -- bulk verify -----------------------------------------------------------
+    def sha1_batch(self, pieces: Sequence) -> list[bytes]:
+        n = len(pieces)
+        ptrs, lens, keep = _ptr_arrays(pieces)
+        out = ctypes.create_string_buffer(20 * max(n, 1))
+        check(lib().vx_sha1_batch(self._h, ptrs, lens, n, out), "vx_sha1_batch")
+        raw = out.raw
+        return [raw[20 * i: 20 * i + 20] for i in range(n)]
+
+    def verify_batch(self, pieces: Sequence, expected: Sequence[bytes]) -> tuple[list[bool], list[bytes]]:
+        n = len(pieces)
+        if len(expected) != n:
+            raise ValueError("expected must have one digest per piece")
+        ptrs, lens, keep = _ptr_arrays(pieces)
+        exp = ctypes.create_string_buffer(b"".join(bytes(e) for e in expected), 20 * max(n, 1))
+        matched = ctypes.create_string_buffer(max(n, 1))
+        dig = ctypes.create_string_buffer(20 * max(n, 1))
+        check(lib().vx_verify_batch(self._h, ptrs, lens, exp, n, matched, dig), "vx_verify_batch")
+        raw = dig.raw
+        return [bool(b) for b in matched.raw[:n]], [raw[20 * i: 20 * i + 20] for i in range(n)]
+
+
+def _ptr_arrays(pieces: Sequence):
+    n = len(pieces)
+    keep = []
+    ptrs = (ctypes.c_void_p * max(n, 1))()
+    lens = (ctypes.c_uint32 * max(n, 1))()
+    for i, p in enumerate(pieces):
+        addr, k = _addr_of(p if len(p) else b"\0")
+        keep.append(k)
+        ptrs[i] = addr
+        lens[i] = len(p)
+    return ptrs, lens, keep
+
+
+def verify_pieces(pieces: Sequence, expected: Sequence[bytes], device: int = 0,
+                  piece_length: Optional[int] = None) -> list[bool]:
+    """torrent.rs:724-740: one verdict per piece, in piece order."""
+    plen = piece_length or max((len(p) for p in pieces), default=1) or 1
+    with HashPool(plen, device=device) as pool:
+        matched, _ = pool.verify_batch(pieces, expected)
+    return matched
+
+
+def piece_len(index: int, num_pieces: int, piece_length: int, total_length: int) -> int:
+    """PieceSelector::piece_len with the last-piece rule (piece_selector.rs:63-69, 291-298)."""
+    last = total_length % piece_length or piece_length
+    return last if index == num_pieces - 1 else piece_length
+
+
+__all__ = ["DownloadedPiece", "HashPool", "verify_pieces", "piece_len"]
