@@ -230,6 +230,11 @@ def main() -> int:
     total_bytes = n_total * plen
     value = total_bytes / elapsed * args.steps / GiB
     achieved = n * plen / (kern_ms * 1e-3)
+    # Integer-VALU ceiling (DESIGN.md "Roofline"): 613.5 VALU per 64-byte block
+    # (measured SQ_INSTS_VALU / waves / blocks), 16 lanes/clk per SIMD for
+    # these VOP3 integer ops, 1,024 SIMDs, nominal 2.4 GHz.
+    valu_ops = n * ((plen + 9 + 63) // 64) * 613.5 / (kern_ms * 1e-3)
+    valu_peak = 256 * 4 * 16 * 2.4e9
     workload = f"{n} x {plen // 1024} KiB pieces per GPU"
     res = {
         "metric": METRIC,
@@ -252,7 +257,10 @@ def main() -> int:
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4),
                      "traffic": load_traffic(workload, n, plen),
                      "kernel": "sha1_uniform_kernel", "kernel_ms": round(kern_ms, 4),
-                     "algorithmic_bytes_per_launch": n * plen},
+                     "algorithmic_bytes_per_launch": n * plen,
+                     "valu": {"achieved_Tops": round(valu_ops / 1e12, 2), "peak_Tops_at_2.4GHz": round(valu_peak / 1e12, 2),
+                              "frac": round(valu_ops / valu_peak, 4),
+                              "note": "the kernel is integer-VALU bound; see DESIGN.md Roofline"}},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, plen)

@@ -1,0 +1,22 @@
+/*
+ * vx_tuning.h — kernel-variant selection for A/B measurement (not part of
+ * the drop-in boundary).  vx_sha1_device_uniform() always runs the default
+ * (best measured) variant; this entry point lets tools/ and tests pin one.
+ *   0 = default, 1 = lane-per-piece (one wave per 64 pieces does loads,
+ *   schedule and rounds), 2 = producer/consumer split (a load+schedule wave
+ *   feeds a rounds-only wave through an LDS ring).
+ */
+#ifndef VX_TUNING_H
+#define VX_TUNING_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
+                                   const void* d_expected, void* d_matched, void* stream, int variant);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

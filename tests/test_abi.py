@@ -12,7 +12,7 @@ from conftest import ROOT
 
 def declared_symbols():
     names = set()
-    for h in ("vx_hash.h", "vx_synth.h"):
+    for h in ("vx_hash.h", "vx_synth.h", "vx_tuning.h"):
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         names |= set(re.findall(r"\b(vx_[a-z0-9_]+)\s*\(", src))
@@ -21,7 +21,7 @@ def declared_symbols():
 
 def test_headers_compile_as_c(tmp_path):
     c = tmp_path / "t.c"
-    c.write_text('#include "vx_hash.h"\n#include "vx_synth.h"\nint main(void){return (int)sizeof(vx_completion) - 32;}\n')
+    c.write_text('#include "vx_hash.h"\n#include "vx_synth.h"\n#include "vx_tuning.h"\nint main(void){return (int)sizeof(vx_completion) - 32;}\n')
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-c", str(c),
                     "-o", str(tmp_path / "t.o")], check=True)
 

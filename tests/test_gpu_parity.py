@@ -40,7 +40,8 @@ def _ragged_upload(torch, dev, pieces, align=16):
                                                                                dtype=torch.int32, device=dev)
 
 
-def test_uniform_lengths_vs_oracle(built, gpu):
+@pytest.mark.parametrize("variant", [1, 2])
+def test_uniform_lengths_vs_oracle(built, gpu, variant):
     import torch
 
     from vortex_amd import device as vdev
@@ -54,7 +55,7 @@ def test_uniform_lengths_vs_oracle(built, gpu):
         clean = oracle.pool_digest_synth(seed, 0, n, plen, threads=THREADS)
         vdev.synth_fill(data, n, plen, stride=stride, seed=seed, corrupt_every=9)
         exp = torch.frombuffer(bytearray(clean), dtype=torch.uint8).to(gpu)
-        dig, matched = vdev.sha1_uniform(data, n, plen, stride=stride, expected=exp)
+        dig, matched = vdev.sha1_uniform(data, n, plen, stride=stride, expected=exp, variant=variant)
         torch.cuda.synchronize()
         want = oracle.pool_digest_synth(seed, 0, n, plen, corrupt_every=9, threads=THREADS)
         assert dig.cpu().numpy().tobytes() == want, plen
@@ -213,7 +214,8 @@ def test_host_batches_ragged(built, gpu):
 
 
 def test_config2_full_65536x256k(built, gpu):
-    """BASELINE config 2: every one of 65,536 digests bit-exact vs the CPU pool."""
+    """BASELINE config 2: every one of 65,536 digests bit-exact vs the CPU pool,
+    for every uniform kernel variant."""
     import torch
 
     from vortex_amd import device as vdev
@@ -221,13 +223,16 @@ def test_config2_full_65536x256k(built, gpu):
     n, plen, seed = 65536, 262144, 0x5EED0002
     data = torch.empty(n * plen, dtype=torch.uint8, device=gpu)
     vdev.synth_fill(data, n, plen, seed=seed, corrupt_every=100)
-    dig, _ = vdev.sha1_uniform(data, n, plen)
-    torch.cuda.synchronize()
-    got = dig.cpu().numpy().tobytes()
+    got = {}
+    for v in (0, 1, 2):
+        dig, _ = vdev.sha1_uniform(data, n, plen, variant=v)
+        torch.cuda.synchronize()
+        got[v] = dig.cpu().numpy().tobytes()
     del data
     torch.cuda.empty_cache()
     want = oracle.pool_digest_synth(seed, 0, n, plen, corrupt_every=100, threads=THREADS)
-    assert got == want
+    for v in (0, 1, 2):
+        assert got[v] == want, v
 
 
 def test_config3_ragged_full(built, gpu):

@@ -33,7 +33,7 @@ EXPORTS = (
     "vx_submit", "vx_flush", "vx_poll", "vx_drain", "vx_pending",
     "vx_sha1_batch", "vx_verify_batch",
     "vx_sha1_device_uniform", "vx_sha1_device_ragged", "vx_sort_order",
-    "vx_synth_fill",
+    "vx_synth_fill", "vx_sha1_device_uniform_variant",
 )
 
 
@@ -80,6 +80,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "vx_sha1_device_uniform": ([vp, c.c_uint64, c.c_uint32, c.c_uint32, vp, vp, vp, vp], c.c_int),
         "vx_sha1_device_ragged": ([vp, vp, vp, vp, c.c_uint32, vp, vp, vp, vp], c.c_int),
         "vx_sort_order": ([vp, c.c_uint32, vp], c.c_int),
+        "vx_sha1_device_uniform_variant": ([vp, c.c_uint64, c.c_uint32, c.c_uint32, vp, vp, vp, vp, c.c_int],
+                                           c.c_int),
         "vx_synth_fill": ([vp, c.c_uint64, c.c_uint32, c.c_uint32, c.c_uint64, c.c_uint64, c.c_uint32, vp],
                           c.c_int),
     }

@@ -11,8 +11,9 @@
 // with its own HIP stream, a device arena, a pinned staging arena and pinned
 // metadata.  Pieces are appended to the filling slot at 256-byte aligned
 // offsets: pieces inside a registered (pinned) host range are DMA'd straight
-// from the caller's buffer at submit time; others are memcpy'd into the
-// slot's pinned stage and moved with one H2D per contiguous run at launch.
+// from the caller's buffer at launch (adjacent pieces coalesced into one
+// copy); others are memcpy'd into the slot's pinned stage at submit and moved
+// with one H2D per contiguous run at launch.
 // A launch is H2D(meta) → kernel → D2H(digests, verdicts) → event; slots on
 // different streams overlap copy and compute.  vx_poll harvests finished
 // slots without blocking.  No internal threads: like the reference's loop,
@@ -32,6 +33,7 @@
 #include "vx_hash.h"
 #include "vx_kernels.h"
 #include "vx_synth.h"
+#include "vx_tuning.h"
 
 namespace {
 
@@ -61,6 +63,11 @@ struct Run {
     uint64_t lo, hi;  // staged byte range [lo, hi) of the arena
 };
 
+struct DirectRun {
+    const uint8_t* host;  // registered (pinned) source of arena bytes [lo, hi)
+    uint64_t lo, hi;
+};
+
 struct Slot {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
@@ -83,6 +90,7 @@ struct Slot {
     uint8_t* d_matched = nullptr;
     std::vector<uint64_t> tags;
     std::vector<Run> runs;
+    std::vector<DirectRun> druns;
     uint32_t n = 0;
     uint64_t bytes = 0;
     bool uniform = true;
@@ -159,6 +167,7 @@ int alloc_slot(Slot& s, uint64_t arena, uint32_t cap) {
 void reset_fill(Slot& s) {
     s.tags.clear();
     s.runs.clear();
+    s.druns.clear();
     s.n = 0;
     s.bytes = 0;
     s.uniform = true;
@@ -172,6 +181,8 @@ int launch_slot(vx_ctx* c, int si) {
         s.state = Slot::FREE;
         return 0;
     }
+    for (const DirectRun& r : s.druns)
+        VX_HIP(hipMemcpyAsync(s.d_arena + r.lo, r.host, r.hi - r.lo, hipMemcpyHostToDevice, s.stream));
     for (const Run& r : s.runs)
         VX_HIP(hipMemcpyAsync(s.d_arena + r.lo, s.h_stage + r.lo, r.hi - r.lo, hipMemcpyHostToDevice, s.stream));
     const uint32_t n = s.n;
@@ -182,7 +193,7 @@ int launch_slot(vx_ctx* c, int si) {
         const uint32_t len = s.h_lens[0];
         const uint64_t stride = align_up(std::max<uint32_t>(len, 1), kAlign);
         e = vx::launch_uniform(s.d_arena, stride, len, n, s.d_digests, s.has_expected ? s.d_expected : nullptr,
-                               s.d_matched, s.stream);
+                               s.d_matched, s.stream, vx::kUniformDefault);
     } else {
         VX_HIP(hipMemcpyAsync(s.d_offsets, s.h_offsets, (size_t)n * 8, hipMemcpyHostToDevice, s.stream));
         VX_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)n * 4, hipMemcpyHostToDevice, s.stream));
@@ -267,7 +278,13 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
     const uint32_t i = s->n;
     if (len) {
         if (is_registered(c, data, len)) {
-            VX_HIP(hipMemcpyAsync(s->d_arena + off, data, len, hipMemcpyHostToDevice, s->stream));
+            // Pinned source: DMA straight from the caller's buffer at launch;
+            // pieces adjacent in host memory AND in the arena share one copy.
+            if (!s->druns.empty() && s->druns.back().hi == off &&
+                s->druns.back().host + (s->druns.back().hi - s->druns.back().lo) == data)
+                s->druns.back().hi = off + len;
+            else
+                s->druns.push_back(DirectRun{data, off, off + len});
         } else {
             std::memcpy(s->h_stage + off, data, len);
             if (!s->runs.empty() && s->runs.back().hi == off)
@@ -503,8 +520,8 @@ int vx_verify_batch(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens,
     return batch_impl(c, ptrs, lens, expected, n, matched_out, digests_out);
 }
 
-int vx_sha1_device_uniform(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
-                           const void* d_expected, void* d_matched, void* stream) {
+int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
+                                   const void* d_expected, void* d_matched, void* stream, int variant) {
     if (n == 0) return 0;
     if (!d_base) return fail(VX_EINVAL, "vx_sha1_device_uniform: NULL base");
     if (!d_digests && !(d_expected && d_matched))
@@ -513,11 +530,17 @@ int vx_sha1_device_uniform(const void* d_base, uint64_t stride, uint32_t len, ui
     if ((reinterpret_cast<uintptr_t>(d_base) & 15) || (stride & 15))
         return fail(VX_EINVAL, "vx_sha1_device_uniform: base and stride must be 16-byte aligned");
     if (n > 1 && stride < len) return fail(VX_EINVAL, "vx_sha1_device_uniform: stride < len");
+    if (variant < 0 || variant > 2) return fail(VX_EINVAL, "vx_sha1_device_uniform: unknown variant");
     hipError_t e = vx::launch_uniform(static_cast<const uint8_t*>(d_base), stride, len, n,
                                       static_cast<uint8_t*>(d_digests), static_cast<const uint8_t*>(d_expected),
-                                      static_cast<uint8_t*>(d_matched), static_cast<hipStream_t>(stream));
-    if (e != hipSuccess) return hip_fail(e, "sha1_uniform_kernel launch");
+                                      static_cast<uint8_t*>(d_matched), static_cast<hipStream_t>(stream), variant);
+    if (e != hipSuccess) return hip_fail(e, "sha1 uniform kernel launch");
     return 0;
+}
+
+int vx_sha1_device_uniform(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
+                           const void* d_expected, void* d_matched, void* stream) {
+    return vx_sha1_device_uniform_variant(d_base, stride, len, n, d_digests, d_expected, d_matched, stream, 0);
 }
 
 int vx_sha1_device_ragged(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,

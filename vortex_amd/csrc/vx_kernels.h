@@ -8,9 +8,19 @@ namespace vx {
 
 constexpr int kBlock = 256;  // 4 waves = one wave per SIMD of a CU
 constexpr int kRing = 3;     // 128-byte groups in the per-lane register ring
+constexpr int kPairBlock = 128;  // split kernel: consumer wave + producer wave
+
+// Uniform-batch kernel variants (vx_tuning.h): 0 = default (best measured),
+// 1 = lane-per-piece (one wave does everything), 2 = producer/consumer split.
+enum UniformVariant { kUniformDefault = 0, kUniformLane = 1, kUniformSplit = 2 };
+constexpr uint32_t kSplitMaxPieces = 16384;  // default picks split at or below this batch size
 
 hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
-                          const uint8_t* expected, uint8_t* matched, hipStream_t stream);
+                          const uint8_t* expected, uint8_t* matched, hipStream_t stream, int variant = 0);
+hipError_t launch_uniform_lane(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
+                               const uint8_t* expected, uint8_t* matched, hipStream_t stream);
+hipError_t launch_uniform_split(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
+                                const uint8_t* expected, uint8_t* matched, hipStream_t stream);
 
 hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens, const uint32_t* order,
                          uint32_t n, uint8_t* digests, const uint8_t* expected, uint8_t* matched,

@@ -35,10 +35,11 @@ def _req(t: torch.Tensor, name: str, dtype=torch.uint8) -> None:
 def sha1_uniform(data: torch.Tensor, n: int, piece_len: int, stride: Optional[int] = None,
                  expected: Optional[torch.Tensor] = None, digests: Optional[torch.Tensor] = None,
                  matched: Optional[torch.Tensor] = None, want_digests: bool = True,
-                 stream: Optional[torch.cuda.Stream] = None):
+                 stream: Optional[torch.cuda.Stream] = None, variant: int = 0):
     """Hash n pieces of piece_len bytes at data[i*stride : i*stride+piece_len].
 
-    Returns (digests [n,20] or None, matched [n] or None).  Enqueue-only."""
+    Returns (digests [n,20] or None, matched [n] or None).  Enqueue-only.
+    variant: 0 = default kernel; 1/2 pin a variant (include/vx_tuning.h)."""
     _req(data, "data")
     stride = piece_len if stride is None else stride
     if n and (n - 1) * stride + piece_len > data.numel():
@@ -52,12 +53,12 @@ def sha1_uniform(data: torch.Tensor, n: int, piece_len: int, stride: Optional[in
             raise ValueError("expected must hold n*20 bytes")
         if matched is None:
             matched = torch.empty((n,), dtype=torch.uint8, device=dev)
-    rc = lib().vx_sha1_device_uniform(
+    rc = lib().vx_sha1_device_uniform_variant(
         data.data_ptr(), stride, piece_len, n,
         digests.data_ptr() if (want_digests and digests is not None) else None,
         expected.data_ptr() if expected is not None else None,
         matched.data_ptr() if expected is not None else None,
-        _stream_ptr(stream, dev))
+        _stream_ptr(stream, dev), variant)
     check(rc, "vx_sha1_device_uniform")
     return (digests if want_digests else None), (matched if expected is not None else None)
 
