@@ -145,6 +145,10 @@ def main() -> int:
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-thread seconds for the baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL on ROCm, the real path) or gloo (single-GPU multi-rank rehearsal)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal only: every rank uses cuda:0 (with --dist-backend gloo)")
     args = ap.parse_args()
 
     import torch
@@ -158,10 +162,15 @@ def main() -> int:
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    if args.same_device:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     n, plen = args.pieces, args.piece_len
     stride = (plen + 15) // 16 * 16
@@ -215,7 +224,8 @@ def main() -> int:
     elapsed = t1 - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
     if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
+                         device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed, kern_ms = float(t[0]), float(t[1])
 

@@ -136,6 +136,21 @@ int vx_sha1_batch(vx_ctx* ctx, const uint8_t* const* ptrs, const uint32_t* lens,
 int vx_verify_batch(vx_ctx* ctx, const uint8_t* const* ptrs, const uint32_t* lens, const uint8_t* expected,
                     size_t n, uint8_t* matched_out, uint8_t* digests_out);
 
+/* ---- bulk re-verify from disk (torrent.rs:716-761, file_store.rs:228-303)
+ * The torrent's files in order (path, length); the layout follows
+ * FileStore::new (file_store.rs:126-160): pieces run across file boundaries,
+ * piece i has piece_length bytes except the last (piece_selector.rs:63-69).
+ * Every piece's segments are pread (io_threads readers, 0 = default) into
+ * pinned batch buffers that stream to the GPU while the next batch is read.
+ * matched_out[i] = 1 iff piece i was read completely and its SHA-1 equals
+ * expected[20*i..].  A piece whose file is missing, short or unreadable is
+ * matched = 0, like the reference's `Err(_) => false` (torrent.rs:731-737).
+ * Returns the number of pieces that hit an I/O error (>= 0) or a VX_E* code.
+ * Requires no async pieces pending on ctx. */
+int64_t vx_verify_files(vx_ctx* ctx, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
+                        uint32_t piece_length, const uint8_t* expected, size_t n_pieces, uint8_t* matched_out,
+                        uint32_t io_threads);
+
 /* ---- device-resident batches (the hot path; no context needed) -------- */
 /* Pieces i in [0,n) at d_base + i*stride, each len bytes.  Writes
  * d_digests[20*i..] (may be NULL) and, when d_expected is given,

@@ -13,6 +13,9 @@
 extern "C" {
 #endif
 
+int vx_sha1_device_ragged_variant(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
+                                  const uint32_t* d_order, uint32_t n, void* d_digests, const void* d_expected,
+                                  void* d_matched, void* stream, int variant);
 int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
                                    const void* d_expected, void* d_matched, void* stream, int variant);
 

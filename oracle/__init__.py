@@ -61,6 +61,10 @@ def lib() -> ctypes.CDLL:
                                             ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
                                             ctypes.c_int, ctypes.c_void_p]
         L.vxo_pool_digest_synth.restype = ctypes.c_int
+        L.vxo_pool_verify_files.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
+                                            ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_void_p]
+        L.vxo_pool_verify_files.restype = ctypes.c_int
         L.vxo_sha1_ctx_size.restype = ctypes.c_size_t
         L.vxo_sha1_init.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.vxo_sha1_update.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
@@ -143,6 +147,19 @@ def pool_digest_synth(seed: int, first: int, n: int, piece_len: int, last_index:
     lib().vxo_pool_digest_synth(seed, first, n, piece_len, last_index, last_len, corrupt_every, threads,
                                 backend, out)
     return out.raw[: 20 * n]
+
+
+def pool_verify_files(paths, file_lengths, piece_length: int, expected: bytes, threads: int = 1,
+                      backend: int = 0) -> list:
+    """C++ restatement of the bulk re-verify (torrent.rs:724-740 over
+    file_store.rs:228-303); the CPU baseline for config 5."""
+    n = len(expected) // 20
+    arr = (ctypes.c_char_p * max(1, len(paths)))(*[p.encode() for p in paths])
+    lens = (ctypes.c_uint64 * max(1, len(file_lengths)))(*file_lengths)
+    exp = ctypes.create_string_buffer(expected, max(1, len(expected)))
+    out = ctypes.create_string_buffer(max(1, n))
+    lib().vxo_pool_verify_files(arr, lens, len(paths), piece_length, exp, n, threads, backend, out)
+    return [bool(b) for b in out.raw[:n]]
 
 
 # ---------------------------------------------------------------- geometry

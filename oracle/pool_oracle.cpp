@@ -149,3 +149,72 @@ int vxo_pool_digest_synth(uint64_t seed, uint64_t first, size_t n, uint32_t piec
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Bulk re-verify from files, restated: State::from_metadata_and_root's
+// par_iter over FileStore::check_piece_hash_sync (torrent.rs:724-740,
+// file_store.rs:228-303).  Per piece: walk the overlapping files, allocate a
+// fresh buffer per segment (file_store.rs:272), pread it fully, feed the
+// hasher; any I/O error or short read -> false (torrent.rs:731-737).
+// ---------------------------------------------------------------------------
+#include <fcntl.h>
+#include <unistd.h>
+
+extern "C" {
+size_t vxo_sha1_ctx_size(void);
+void vxo_sha1_init(void* c, int backend);
+void vxo_sha1_update(void* c, const uint8_t* p, size_t n);
+void vxo_sha1_final(void* c, uint8_t out[20]);
+
+int vxo_pool_verify_files(const char* const* paths, const uint64_t* lens, size_t nfiles, uint32_t piece_length,
+                          const uint8_t* expected, size_t n, int threads, int backend, uint8_t* matched_out) {
+    struct Span { int64_t sp, so, ep, eo, len; };
+    std::vector<Span> fs;
+    int64_t sp = 0, so = 0;
+    for (size_t f = 0; f < nfiles; ++f) {  // FileStore::new, file_store.rs:126-160
+        const int64_t L = (int64_t)lens[f];
+        fs.push_back(Span{sp, so, sp + (L + so) / piece_length, (L + so) % piece_length, L});
+        sp = fs.back().ep;
+        so = fs.back().eo;
+    }
+    std::vector<int> fds(nfiles);
+    for (size_t f = 0; f < nfiles; ++f) fds[f] = open(paths[f], O_RDONLY | O_CLOEXEC);
+    Mpsc ch;
+    std::vector<uint8_t> result(n, 0);
+    auto job = [&](size_t idx) {
+        DownloadedPiece p;
+        p.index = idx;
+        std::vector<uint8_t> ctx(vxo_sha1_ctx_size());
+        vxo_sha1_init(ctx.data(), backend);
+        const int64_t piece = (int64_t)idx;
+        int64_t total = 0;
+        bool ok = true;
+        for (size_t f = 0; f < fs.size() && ok; ++f) {
+            const Span& s = fs[f];
+            if (!(s.sp <= piece && piece <= s.ep)) continue;
+            const int64_t off = (piece - s.sp) * (int64_t)piece_length - s.so + total;
+            const int64_t to_read =
+                piece == s.ep ? s.eo - total : std::min<int64_t>((int64_t)piece_length - total, s.len);
+            if (to_read <= 0) continue;
+            std::vector<uint8_t> buffer((size_t)to_read);  // vec![0u8; to_read]
+            int64_t got = 0;
+            while (got < to_read && ok) {
+                const ssize_t r = fds[f] < 0 ? -1 : pread(fds[f], buffer.data() + got, (size_t)(to_read - got), off + got);
+                if (r <= 0) ok = false;
+                else got += r;
+            }
+            if (ok) vxo_sha1_update(ctx.data(), buffer.data(), buffer.size());
+            total += to_read;
+        }
+        vxo_sha1_final(ctx.data(), p.digest);
+        p.hash_matched = ok && std::memcmp(p.digest, expected + 20 * idx, 20) == 0;
+        result[idx] = p.hash_matched ? 1 : 0;
+        return p;
+    };
+    run_pool(n, threads, job, ch);
+    for (int fd : fds)
+        if (fd >= 0) close(fd);
+    std::memcpy(matched_out, result.data(), n);
+    return 0;
+}
+}  // extern "C"

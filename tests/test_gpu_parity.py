@@ -317,3 +317,78 @@ def test_idempotent_and_stream_ordering(built, gpu):
     s.synchronize()
     assert torch.equal(a, b)
     assert a.cpu().numpy().tobytes() == oracle.pool_digest_synth(1, 0, n, plen, threads=THREADS)
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+def test_ragged_variants_vs_oracle(built, gpu, variant):
+    """Both ragged kernels on a mixed batch (0..4 MiB, odd lengths), lane order
+    sorted and unsorted, with verdicts."""
+    import torch
+
+    from vortex_amd import device as vdev
+
+    rng = random.Random(variant)
+    lens = [rng.choice([0, 1, 55, 56, 63, 64, 65, 119, 120, 128, 164, 4096, 16384, 262144 + 7, 1 << 20, 4 << 20])
+            for _ in range(300)]
+    pieces = [oracle.gen_piece(21, i, L) for i, L in enumerate(lens)]
+    d, offs, dlens = _ragged_upload(torch, gpu, pieces)
+    want = [hashlib.sha1(p).digest() for p in pieces]
+    exp_l = list(want)
+    for i in range(0, 300, 7):
+        exp_l[i] = bytes(20)
+    exp = torch.frombuffer(bytearray(b"".join(exp_l)), dtype=torch.uint8).to(gpu)
+    for order in (None, vdev.length_order(lens).to(gpu)):
+        dig, matched = vdev.sha1_ragged(d, offs, dlens, order=order, expected=exp, variant=variant)
+        torch.cuda.synchronize()
+        raw = dig.cpu().numpy().tobytes()
+        assert [raw[20 * i:20 * i + 20] for i in range(300)] == want
+        assert [bool(x) for x in matched.cpu().numpy()] == [i % 7 != 0 for i in range(300)]
+
+
+def test_verify_files_multi_file(built, gpu, tmp_path, golden):
+    """vx_verify_files vs the bulk re-verify restatement: the reference's
+    3-file seeding layout, then a ragged 9-file layout with a missing file, a
+    truncated file and a corrupted byte (torrent.rs:724-740, file_store.rs:228-303)."""
+    from vortex_amd.hash_pool import HashPool
+
+    st = golden["setup_seeding_test"]
+    paths, lens = [], []
+    for k, f in enumerate(st["files"]):
+        p = tmp_path / f"f{k + 1}.txt"
+        p.write_bytes(bytes([f["byte"]]) * f["len"])
+        paths.append(str(p))
+        lens.append(f["len"])
+    exp = b"".join(bytes.fromhex(h) for h in st["pieces"])
+    with HashPool(st["piece_length"]) as pool:
+        got, bad = pool.verify_files(paths, lens, st["piece_length"], exp)
+    assert got == [True] * 9 and bad == 0
+
+    sizes = [5, 0, 70000, 1 << 20, 12345, 3 << 20, 64, 999999, 2 << 20]
+    pl = 256 * 1024
+    d2 = tmp_path / "t2"
+    d2.mkdir()
+    paths = []
+    for k, L in enumerate(sizes):
+        p = d2 / f"part{k}.bin"
+        p.write_bytes(oracle.gen_piece(8, k, L))
+        paths.append(str(p))
+    data = b"".join(open(p, "rb").read() for p in paths)
+    exp = b"".join(hashlib.sha1(data[i:i + pl]).digest() for i in range(0, len(data), pl))
+    n = len(exp) // 20
+    with HashPool(pl, slots=2, batch_pieces=8, slot_bytes=4 << 20) as pool:
+        got, bad = pool.verify_files(paths, sizes, pl, exp, io_threads=4)
+        assert got == [True] * n and bad == 0
+        with open(paths[3], "r+b") as f:  # corrupt one byte of file 3
+            f.seek(777)
+            b = f.read(1)
+            f.seek(777)
+            f.write(bytes([b[0] ^ 0xFF]))
+        with open(paths[5], "r+b") as f:
+            f.truncate(1 << 20)
+        os.unlink(paths[7])
+        got, bad = pool.verify_files(paths, sizes, pl, exp, io_threads=4)
+    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
+    assert got == want
+    assert not all(got) and any(got)
+    assert bad == sum(1 for i in range(n) if any(fi in (5, 7) and (fi == 7 or off + ln > (1 << 20))
+                                                 for fi, off, ln in oracle.piece_segments(i, sizes, pl)))

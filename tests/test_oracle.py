@@ -116,3 +116,42 @@ def test_pool_digest_synth_matches_generator():
         g = 100 + i
         L = 77 if g == 132 else plen
         assert got[20 * i:20 * i + 20] == hashlib.sha1(oracle.gen_piece(0x5EED0002, g, L, 10)).digest()
+
+
+def _write_files(tmp_path, sizes, seed=3):
+    paths = []
+    for k, L in enumerate(sizes):
+        p = tmp_path / f"file{k}.bin"
+        p.write_bytes(oracle.gen_piece(seed, k, L))
+        paths.append(str(p))
+    return paths
+
+
+def _expected_from_concat(paths, sizes, pl):
+    data = b"".join(open(p, "rb").read() for p in paths)
+    assert len(data) == sum(sizes)
+    return b"".join(hashlib.sha1(data[i:i + pl]).digest() for i in range(0, len(data), pl))
+
+
+def test_pool_verify_files_restatement(tmp_path):
+    """The C++ bulk re-verify restatement agrees with the per-piece Python
+    restatement of check_piece_hash_sync, including missing/short files."""
+    sizes = [64, 100, 0, 5000, 32768, 3, 40000]
+    pl = 4096
+    paths = _write_files(tmp_path, sizes)
+    exp = _expected_from_concat(paths, sizes, pl)
+    n = len(exp) // 20
+    got = oracle.pool_verify_files(paths, sizes, pl, exp, threads=3)
+    assert got == [True] * n
+    want = [oracle.check_piece_hash_sync(paths, sizes, pl, i, exp[20 * i:20 * i + 20]) for i in range(n)]
+    assert want == got
+    # truncate file 4 and delete file 6: pieces touching them turn false
+    with open(paths[4], "r+b") as f:
+        f.truncate(30000)
+    os.unlink(paths[6])
+    got = oracle.pool_verify_files(paths, sizes, pl, exp, threads=3)
+    spans = {i: {fi for fi, _, _ in oracle.piece_segments(i, sizes, pl)} for i in range(n)}
+    for i in range(n):
+        touches_bad = 6 in spans[i] or any(fi == 4 and off + ln > 30000 for fi, off, ln in
+                                          oracle.piece_segments(i, sizes, pl))
+        assert got[i] == (not touches_bad), i

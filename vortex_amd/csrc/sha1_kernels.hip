@@ -347,6 +347,116 @@ hipError_t launch_uniform_split(const uint8_t* base, uint64_t stride, uint32_t l
     return hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------
+// Ragged producer/consumer kernel: per-lane offsets/lengths, same two-wave
+// split as sha1_split_kernel.  The wave-uniform trip count is the wave's
+// longest piece (in blocks incl. padding); the producer feeds every lane
+// data blocks, then its 1-2 padding blocks, then zeros, and the consumer
+// commits a block's result only for lanes still inside their piece (a
+// v_cndmask select, no divergent rounds).  Pieces should arrive sorted by
+// descending length (vx_sort_order) so each wave's lanes finish together.
+// ---------------------------------------------------------------------------
+constexpr int kBlockRing = 6;  // 64-byte blocks of loads in flight per lane
+
+__device__ __forceinline__ void load_block(uint4 (&dst)[4], const uint4* src) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[k] = src[k];
+}
+
+// Words of padding block k (0 or 1) of a piece whose tail has `rem` bytes at q.
+__device__ __forceinline__ void pad_words(uint32_t (&w)[16], const uint8_t* q, uint32_t rem, uint64_t len,
+                                          uint32_t k) {
+    const uint32_t bits_hi = (uint32_t)((len * 8u) >> 32);
+    const uint32_t bits_lo = (uint32_t)(len * 8u);
+    if (k == 0) {
+        tail_words(w, q, rem);
+        if (rem <= 55) {
+            w[14] = bits_hi;
+            w[15] = bits_lo;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = 0;
+        if (k == 1 && rem > 55) {
+            w[14] = bits_hi;
+            w[15] = bits_lo;
+        }
+    }
+}
+
+__global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
+    const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lens,
+    const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ digests,
+    const uint8_t* __restrict__ expected, uint8_t* __restrict__ matched) {
+    __shared__ SplitLds lds;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t j = blockIdx.x * 64 + lane;
+    const uint32_t jj = j < n ? j : n - 1;
+    const uint32_t idx = order ? order[jj] : jj;
+    const uint32_t len = lens[idx];
+    const uint8_t* p = base + offsets[idx];
+    const uint32_t nfull = len >> 6;
+    const uint32_t rem = len & 63u;
+    const uint32_t nb = nfull + (rem <= 55 ? 1u : 2u);
+    const uint32_t nb_wave = __builtin_amdgcn_readfirstlane(wave_max(nb));
+
+    if (wave == 1) {
+        // ---------------- producer ----------------
+        constexpr int R = kBlockRing;
+        const uint4* src = nfull ? reinterpret_cast<const uint4*>(p) : g_zero_line;
+        const uint32_t last = nfull ? nfull - 1 : 0;
+        const uint8_t* q = p + (size_t)nfull * 64;
+        uint4 ring[R][4];
+        uint32_t w[16];
+#pragma unroll
+        for (int r = 0; r < R - 1; ++r) {
+            const uint32_t bl = (uint32_t)r < last ? (uint32_t)r : last;
+            load_block(ring[r], src + (size_t)bl * 4);
+        }
+        for (uint32_t b0 = 0; b0 < nb_wave; b0 += R) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t b = b0 + r;
+                const uint32_t bl_raw = b + R - 1;
+                const uint32_t bl = bl_raw < last ? bl_raw : last;
+                load_block(ring[(r + R - 1) % R], src + (size_t)bl * 4);
+                if (b < nb_wave) {
+                    if (b < nfull) {
+                        le_words(w, ring[r][0], ring[r][1], ring[r][2], ring[r][3]);
+                    } else {
+                        pad_words(w, q, rem, len, b - nfull);
+                    }
+                    expand_store(w, lds.w[b & 1], lane);
+                    __syncthreads();
+                }
+            }
+        }
+        __syncthreads();
+    } else {
+        // ---------------- consumer ----------------
+        State s = iv();
+        __syncthreads();
+        for (uint32_t b = 0; b < nb_wave; ++b) {
+            State t = s;
+            rounds_lds(t, lds.w[b & 1], lane);
+            if (b < nb) s = t;
+            __syncthreads();
+        }
+        if (j < n) emit(s, idx, digests, expected, matched);
+    }
+}
+
+hipError_t launch_ragged_split(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens,
+                               const uint32_t* order, uint32_t n, uint8_t* digests, const uint8_t* expected,
+                               uint8_t* matched, hipStream_t stream) {
+    const uint32_t blocks = (n + 63) / 64;
+    hipLaunchKernelGGL(sha1_ragged_split_kernel, dim3(blocks), dim3(kPairBlock), 0, stream, base, offsets, lens,
+                       order, n, digests, expected, matched);
+    return hipGetLastError();
+}
+
 hipError_t launch_uniform_lane(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
                           const uint8_t* expected, uint8_t* matched, hipStream_t stream) {
     const uint32_t blocks = (n + kBlock - 1) / kBlock;
@@ -355,9 +465,9 @@ hipError_t launch_uniform_lane(const uint8_t* base, uint64_t stride, uint32_t le
     return hipGetLastError();
 }
 
-hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens, const uint32_t* order,
-                         uint32_t n, uint8_t* digests, const uint8_t* expected, uint8_t* matched,
-                         hipStream_t stream) {
+hipError_t launch_ragged_lane(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens,
+                              const uint32_t* order, uint32_t n, uint8_t* digests, const uint8_t* expected,
+                              uint8_t* matched, hipStream_t stream) {
     const uint32_t blocks = (n + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(sha1_ragged_kernel, dim3(blocks), dim3(kBlock), 0, stream, base, offsets, lens, order, n,
                        digests, expected, matched);
@@ -378,5 +488,18 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, ui
     // block) finishes each piece sooner (DESIGN.md "Kernels", measured).
     if (n <= kSplitMaxPieces) return launch_uniform_split(base, stride, len, n, digests, expected, matched, stream);
     return launch_uniform_lane(base, stride, len, n, digests, expected, matched, stream);
+}
+}  // namespace vx
+
+namespace vx {
+hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens, const uint32_t* order,
+                         uint32_t n, uint8_t* digests, const uint8_t* expected, uint8_t* matched,
+                         hipStream_t stream, int variant) {
+    if (variant == kUniformLane) return launch_ragged_lane(base, offsets, lens, order, n, digests, expected, matched, stream);
+    if (variant == kUniformSplit)
+        return launch_ragged_split(base, offsets, lens, order, n, digests, expected, matched, stream);
+    if (n <= kSplitMaxPieces)
+        return launch_ragged_split(base, offsets, lens, order, n, digests, expected, matched, stream);
+    return launch_ragged_lane(base, offsets, lens, order, n, digests, expected, matched, stream);
 }
 }  // namespace vx

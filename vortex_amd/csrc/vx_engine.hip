@@ -543,9 +543,9 @@ int vx_sha1_device_uniform(const void* d_base, uint64_t stride, uint32_t len, ui
     return vx_sha1_device_uniform_variant(d_base, stride, len, n, d_digests, d_expected, d_matched, stream, 0);
 }
 
-int vx_sha1_device_ragged(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
-                          const uint32_t* d_order, uint32_t n, void* d_digests, const void* d_expected,
-                          void* d_matched, void* stream) {
+int vx_sha1_device_ragged_variant(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
+                                  const uint32_t* d_order, uint32_t n, void* d_digests, const void* d_expected,
+                                  void* d_matched, void* stream, int variant) {
     if (n == 0) return 0;
     if (!d_base || !d_offsets || !d_lens) return fail(VX_EINVAL, "vx_sha1_device_ragged: NULL argument");
     if (!d_digests && !(d_expected && d_matched))
@@ -553,11 +553,19 @@ int vx_sha1_device_ragged(const void* d_base, const uint64_t* d_offsets, const u
     if (d_matched && !d_expected) return fail(VX_EINVAL, "vx_sha1_device_ragged: d_matched needs d_expected");
     if (reinterpret_cast<uintptr_t>(d_base) & 15)
         return fail(VX_EINVAL, "vx_sha1_device_ragged: base must be 16-byte aligned");
+    if (variant < 0 || variant > 2) return fail(VX_EINVAL, "vx_sha1_device_ragged: unknown variant");
     hipError_t e = vx::launch_ragged(static_cast<const uint8_t*>(d_base), d_offsets, d_lens, d_order, n,
                                      static_cast<uint8_t*>(d_digests), static_cast<const uint8_t*>(d_expected),
-                                     static_cast<uint8_t*>(d_matched), static_cast<hipStream_t>(stream));
-    if (e != hipSuccess) return hip_fail(e, "sha1_ragged_kernel launch");
+                                     static_cast<uint8_t*>(d_matched), static_cast<hipStream_t>(stream), variant);
+    if (e != hipSuccess) return hip_fail(e, "sha1 ragged kernel launch");
     return 0;
+}
+
+int vx_sha1_device_ragged(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
+                          const uint32_t* d_order, uint32_t n, void* d_digests, const void* d_expected,
+                          void* d_matched, void* stream) {
+    return vx_sha1_device_ragged_variant(d_base, d_offsets, d_lens, d_order, n, d_digests, d_expected, d_matched,
+                                         stream, 0);
 }
 
 int vx_sort_order(const uint32_t* lens, uint32_t n, uint32_t* order_out) {

@@ -24,7 +24,13 @@ hipError_t launch_uniform_split(const uint8_t* base, uint64_t stride, uint32_t l
 
 hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens, const uint32_t* order,
                          uint32_t n, uint8_t* digests, const uint8_t* expected, uint8_t* matched,
-                         hipStream_t stream);
+                         hipStream_t stream, int variant = 0);
+hipError_t launch_ragged_lane(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens,
+                              const uint32_t* order, uint32_t n, uint8_t* digests, const uint8_t* expected,
+                              uint8_t* matched, hipStream_t stream);
+hipError_t launch_ragged_split(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens,
+                               const uint32_t* order, uint32_t n, uint8_t* digests, const uint8_t* expected,
+                               uint8_t* matched, hipStream_t stream);
 
 hipError_t launch_synth_fill(uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint64_t first,
                              uint64_t seed, uint32_t corrupt_every, hipStream_t stream);

@@ -66,11 +66,12 @@ def sha1_uniform(data: torch.Tensor, n: int, piece_len: int, stride: Optional[in
 def sha1_ragged(data: torch.Tensor, offsets: torch.Tensor, lens: torch.Tensor,
                 order: Optional[torch.Tensor] = None, expected: Optional[torch.Tensor] = None,
                 digests: Optional[torch.Tensor] = None, matched: Optional[torch.Tensor] = None,
-                stream: Optional[torch.cuda.Stream] = None):
+                stream: Optional[torch.cuda.Stream] = None, variant: int = 0):
     """Hash piece i = data[offsets[i] : offsets[i]+lens[i]] for all i.
 
     offsets: int64 device tensor (16-byte aligned values); lens: int32 device
-    tensor; order: optional int32 permutation (see :func:`length_order`)."""
+    tensor; order: optional int32 permutation (see :func:`length_order`).
+    variant: 0 = default kernel; 1 lane / 2 split pin one (vx_tuning.h)."""
     _req(data, "data")
     _req(offsets, "offsets", torch.int64)
     _req(lens, "lens", torch.int32)
@@ -86,12 +87,12 @@ def sha1_ragged(data: torch.Tensor, offsets: torch.Tensor, lens: torch.Tensor,
             matched = torch.empty((n,), dtype=torch.uint8, device=dev)
     if order is not None:
         _req(order, "order", torch.int32)
-    rc = lib().vx_sha1_device_ragged(
+    rc = lib().vx_sha1_device_ragged_variant(
         data.data_ptr(), offsets.data_ptr(), lens.data_ptr(),
         order.data_ptr() if order is not None else None, n, digests.data_ptr(),
         expected.data_ptr() if expected is not None else None,
         matched.data_ptr() if expected is not None else None,
-        _stream_ptr(stream, dev))
+        _stream_ptr(stream, dev), variant)
     check(rc, "vx_sha1_device_ragged")
     return digests, matched
 

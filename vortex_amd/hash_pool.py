@@ -28,6 +28,7 @@ All hashing runs in libvortex_amd.so on the GPU; there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Any, Iterable, Optional, Sequence
 
@@ -184,6 +185,14 @@ class HashPool:
         raw = out.raw
         return [raw[20 * i: 20 * i + 20] for i in range(n)]
 
+    def verify_files(self, paths: Sequence[str], file_lengths: Sequence[int], piece_length: int,
+                     expected: bytes, io_threads: int = 0) -> tuple[list[bool], int]:
+        """State::from_metadata_and_root's bulk re-verify (torrent.rs:716-761):
+        pieces read from the torrent's files (file_store.rs:228-303 byte
+        ranges) and verified on the GPU.  Returns (verdicts, pieces with I/O
+        errors).  `expected` is the torrent's `pieces` string (n*20 bytes)."""
+        return _verify_files(self, paths, file_lengths, piece_length, expected, io_threads)
+
     def verify_batch(self, pieces: Sequence, expected: Sequence[bytes]) -> tuple[list[bool], list[bytes]]:
         n = len(pieces)
         if len(expected) != n:
@@ -195,6 +204,18 @@ class HashPool:
         check(lib().vx_verify_batch(self._h, ptrs, lens, exp, n, matched, dig), "vx_verify_batch")
         raw = dig.raw
         return [bool(b) for b in matched.raw[:n]], [raw[20 * i: 20 * i + 20] for i in range(n)]
+
+
+def _verify_files(pool: "HashPool", paths: Sequence[str], file_lengths: Sequence[int], piece_length: int,
+                  expected: bytes, io_threads: int = 0) -> tuple[list[bool], int]:
+    n = len(expected) // 20
+    arr = (ctypes.c_char_p * max(1, len(paths)))(*[os.fsencode(p) for p in paths])
+    lens = (ctypes.c_uint64 * max(1, len(file_lengths)))(*file_lengths)
+    exp = ctypes.create_string_buffer(bytes(expected), max(1, len(expected)))
+    out = ctypes.create_string_buffer(max(1, n))
+    bad = check(lib().vx_verify_files(pool._h, arr, lens, len(paths), piece_length, exp, n, out, io_threads),
+                "vx_verify_files")
+    return [bool(b) for b in out.raw[:n]], int(bad)
 
 
 def _ptr_arrays(pieces: Sequence):

@@ -55,9 +55,14 @@ def gather_verdicts(matched_local: torch.Tensor, n_total: int, group=None) -> to
     width = max(counts)
     if matched_local.numel() != counts[rank]:
         raise ValueError("local verdicts do not match this rank's shard")
-    padded = torch.zeros(width, dtype=torch.uint8, device=matched_local.device)
-    padded[: counts[rank]] = matched_local
-    out = torch.empty(world * width, dtype=torch.uint8, device=matched_local.device)
+    # gloo (CPU tests, single-GPU rehearsals) gathers host tensors; RCCL gathers
+    # device tensors in place over xGMI.
+    dev = matched_local.device
+    on_host = dist.get_backend(group) == "gloo"
+    work_dev = torch.device("cpu") if on_host else dev
+    padded = torch.zeros(width, dtype=torch.uint8, device=work_dev)
+    padded[: counts[rank]] = matched_local.to(work_dev)
+    out = torch.empty(world * width, dtype=torch.uint8, device=work_dev)
     dist.all_gather_into_tensor(out, padded, group=group)
     parts = [out[r * width: r * width + counts[r]] for r in range(world)]
-    return torch.cat(parts)
+    return torch.cat(parts).to(dev)
