@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--keep", action="store_true")
+    ap.add_argument("--slots", type=int, default=4)
+    ap.add_argument("--slot-mib", type=int, default=512)
     a = ap.parse_args()
     import ctypes
 
@@ -54,7 +56,7 @@ def main():
     res = {"workload": f"re-verify {n} x 2 MiB pieces ({total} B, linux-mint geometry) from a file",
            "file_bytes": total, "write_s": round(t_write, 2), "threads": threads, "runs": []}
     GiB = float(1 << 30)
-    with HashPool(pl, slots=4, slot_bytes=256 << 20, batch_pieces=128) as pool:
+    with HashPool(pl, slots=a.slots, slot_bytes=a.slot_mib << 20, batch_pieces=4096) as pool:
         for rep in range(a.reps):
             t0 = time.perf_counter()
             got, bad = pool.verify_files([path], [total], pl, exp, io_threads=threads)

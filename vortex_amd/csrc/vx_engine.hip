@@ -20,6 +20,9 @@
 // everything is driven from the caller's thread.
 #include <hip/hip_runtime.h>
 
+#include <fcntl.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstring>
@@ -30,6 +33,7 @@
 #include <thread>
 #include <vector>
 
+#include "vx_files.hpp"
 #include "vx_hash.h"
 #include "vx_kernels.h"
 #include "vx_synth.h"
@@ -518,6 +522,100 @@ int vx_verify_batch(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens,
                     uint8_t* matched_out, uint8_t* digests_out) {
     if (n && (!expected || !matched_out)) return fail(VX_EINVAL, "vx_verify_batch: NULL expected/matched_out");
     return batch_impl(c, ptrs, lens, expected, n, matched_out, digests_out);
+}
+
+
+// Bulk re-verify from disk (include/vx_hash.h).  The reader threads pread
+// each slot's pieces straight into that slot's pinned stage (segments back
+// to back, file_store.rs:240-298 byte ranges), then the slot launches
+// (one H2D run, kernel, D2H verdicts) while the next free slot is read.
+// Completions are consumed here; they never reach vx_poll.
+int64_t vx_verify_files(vx_ctx* c, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
+                        uint32_t piece_length, const uint8_t* expected, size_t n_pieces, uint8_t* matched_out,
+                        uint32_t io_threads) {
+    if (!c || (nfiles && (!paths || !file_lengths)) || piece_length == 0 || (n_pieces && (!expected || !matched_out)))
+        return fail(VX_EINVAL, "vx_verify_files: bad argument");
+    if (c->sticky) return c->sticky;
+    if (c->pending || c->filling >= 0) return fail(VX_EBUSY, "vx_verify_files: async pieces pending");
+    if (piece_length > c->cfg.max_piece_len) return fail(VX_ERANGE, "vx_verify_files: piece_length > max_piece_len");
+    uint64_t total = 0;
+    for (size_t f = 0; f < nfiles; ++f) total += file_lengths[f];
+    if (n_pieces != (total + piece_length - 1) / piece_length)
+        return fail(VX_EINVAL, "vx_verify_files: n_pieces does not match the files' total length");
+    if (n_pieces == 0) return 0;
+    int rc = set_device(c);
+    if (rc) return rc;
+
+    const std::vector<vx_files::FileSpan> fs = vx_files::layout(file_lengths, nfiles, piece_length);
+    std::vector<int> fds(nfiles, -1);
+    for (size_t f = 0; f < nfiles; ++f) fds[f] = open(paths[f], O_RDONLY | O_CLOEXEC);
+    const int nthreads = io_threads ? (int)io_threads
+                                    : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<uint8_t> bad(n_pieces, 0);
+    std::memset(matched_out, 0, n_pieces);
+    const uint64_t stride = align_up(piece_length, kAlign);
+    uint64_t next = 0, done = 0;
+    {
+        vx_files::Readers rd(nthreads, fs, fds, piece_length, n_pieces, total);
+        auto consume = [&]() {
+            while (!c->done.empty()) {
+                const vx_completion& r = c->done.front();
+                matched_out[r.tag] = (r.matched && !bad[r.tag]) ? 1 : 0;
+                c->done.pop_front();
+                ++done;
+            }
+        };
+        while (done < n_pieces && !rc) {
+            int si = -1;
+            if (next < n_pieces)
+                for (int k = 0; k < (int)c->slots.size(); ++k)
+                    if (c->slots[k].state == Slot::FREE) {
+                        si = k;
+                        break;
+                    }
+            if (si < 0) {  // nothing to read into: wait for the oldest batch
+                rc = reap(c, true);
+                consume();
+                continue;
+            }
+            Slot& s = c->slots[si];
+            reset_fill(s);
+            const uint64_t cap = std::min<uint64_t>(s.cap, std::max<uint64_t>(1, s.arena_cap / stride));
+            const uint64_t lo = next, hi = std::min<uint64_t>(n_pieces, next + cap);
+            rd.start(lo, hi, s.h_stage, stride, bad.data());
+            rd.wait();
+            for (uint64_t i = lo; i < hi; ++i) {
+                const uint32_t k = (uint32_t)(i - lo);
+                s.h_offsets[k] = k * stride;
+                s.h_lens[k] = rd.piece_len(i);
+                if (s.h_lens[k] != s.h_lens[0]) s.uniform = false;
+                std::memcpy(s.h_expected + (size_t)k * 20, expected + 20 * i, 20);
+                s.tags.push_back(i);
+            }
+            s.n = (uint32_t)(hi - lo);
+            s.has_expected = true;
+            s.bytes = (hi - lo - 1) * stride + s.h_lens[s.n - 1];
+            s.runs.push_back(Run{0, s.bytes});
+            s.state = Slot::FILLING;
+            rc = launch_slot(c, si);
+            next = hi;
+            if (!rc) rc = reap(c, false);
+            consume();
+        }
+        if (rc) {
+            for (auto& s : c->slots)
+                if (s.state == Slot::INFLIGHT) (void)hipEventSynchronize(s.done);
+            for (auto& s : c->slots)
+                if (s.state == Slot::INFLIGHT) harvest(c, s);
+            c->done.clear();
+        }
+    }
+    for (int fd : fds)
+        if (fd >= 0) close(fd);
+    if (rc) return rc;
+    int64_t nbad = 0;
+    for (uint8_t x : bad) nbad += x;
+    return nbad;
 }
 
 int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
