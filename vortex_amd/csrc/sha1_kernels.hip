@@ -69,11 +69,11 @@ __device__ __forceinline__ void stream_groups(State& s, const uint4* src, uint32
     }
 }
 
-template <bool kUniform>
+template <bool kUniform, int R = kRing>
 __device__ __forceinline__ void hash_piece(State& s, const uint8_t* p, uint32_t len, uint32_t ng_wave) {
     const uint32_t nfull = len >> 6;
     const uint32_t ng = nfull >> 1;
-    stream_groups<kRing, kUniform>(s, reinterpret_cast<const uint4*>(p), ng, ng_wave);
+    stream_groups<R, kUniform>(s, reinterpret_cast<const uint4*>(p), ng, ng_wave);
     const uint8_t* q = p + (size_t)ng * 128;
     if (nfull & 1) {
         const uint4* q4 = reinterpret_cast<const uint4*>(q);
@@ -110,6 +110,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
     return v;
 }
 
+template <int R, bool kAlias = false>
 __global__ __launch_bounds__(kBlock) void sha1_uniform_kernel(const uint8_t* __restrict__ base, uint64_t stride,
                                                               uint32_t len, uint32_t n,
                                                               uint8_t* __restrict__ digests,
@@ -118,9 +119,9 @@ __global__ __launch_bounds__(kBlock) void sha1_uniform_kernel(const uint8_t* __r
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     // Lanes past n re-hash piece n-1 (in bounds, wave stays convergent) and
     // store nothing.
-    const uint32_t pi = i < n ? i : n - 1;
+    const uint32_t pi = kAlias ? 0 : (i < n ? i : n - 1);  // kAlias: diagnostic, every lane reads piece 0
     State s = iv();
-    hash_piece<true>(s, base + (size_t)pi * stride, len, (len >> 7));
+    hash_piece<true, R>(s, base + (size_t)pi * stride, len, (len >> 7));
     if (i < n) emit(s, i, digests, expected, matched);
 }
 
@@ -457,12 +458,18 @@ hipError_t launch_ragged_split(const uint8_t* base, const uint64_t* offsets, con
     return hipGetLastError();
 }
 
-hipError_t launch_uniform_lane(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
-                          const uint8_t* expected, uint8_t* matched, hipStream_t stream) {
+template <int R, bool kAlias = false>
+hipError_t launch_uniform_lane_r(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
+                                 const uint8_t* expected, uint8_t* matched, hipStream_t stream) {
     const uint32_t blocks = (n + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(sha1_uniform_kernel, dim3(blocks), dim3(kBlock), 0, stream, base, stride, len, n, digests,
+    hipLaunchKernelGGL((sha1_uniform_kernel<R, kAlias>), dim3(blocks), dim3(kBlock), 0, stream, base, stride, len, n, digests,
                        expected, matched);
     return hipGetLastError();
+}
+
+hipError_t launch_uniform_lane(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
+                               const uint8_t* expected, uint8_t* matched, hipStream_t stream) {
+    return launch_uniform_lane_r<kRing>(base, stride, len, n, digests, expected, matched, stream);
 }
 
 hipError_t launch_ragged_lane(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens,
