@@ -1,0 +1,216 @@
+// loop_harness.cpp — test harness: vortex's download-path control flow driven
+// against the C ABI (include/vx_hash.h), without io_uring or sockets.
+//
+// What it mirrors (reference file:line):
+//  * BufferPool of piece_length page-aligned mmap buffers, MAP_POPULATE
+//    (torrent.rs:344, buf_pool.rs:92-133, buf_ring.rs:24-42) — registered
+//    with vx_register_host_buffer so completed pieces DMA straight to the GPU.
+//  * Piece::on_subpiece copies each 16 KiB subpiece into the piece buffer
+//    (piece_selector.rs:381-398); when the piece is complete it is handed to
+//    the hasher (peer_connection.rs:1122-1158) → vx_submit.
+//  * Once per loop turn the event loop drains completions
+//    (event_loop.rs:554-557 → torrent.rs:415-442) → vx_flush + vx_poll:
+//    match → piece complete (buffer returned after the "disk write");
+//    mismatch → mark_not_downloaded + return_buffer + re-request.
+//  * Buffers are reused without zeroing (buf_pool.rs:148-157); the engine
+//    must hash exactly piece_len bytes.
+// "Peers" deliver subpieces of synthetic data (DESIGN.md "Synthetic pieces");
+// a configurable fraction of first deliveries is corrupted, so the mismatch
+// branch runs and the piece is downloaded again.
+//
+// usage: loop_harness <expected.bin> <n_pieces> <piece_len> <last_len> <seed>
+//                     [peers=32] [subpieces_per_turn=4] [corrupt_every=50]
+// prints one JSON line; exit status 0 iff every piece completed with the
+// expected digest and every corrupted delivery was rejected.
+#include <sys/mman.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <unordered_map>
+#include <vector>
+
+#include "vx_hash.h"
+
+namespace {
+
+uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+// Synthetic piece bytes [off, off+len) of piece p.
+void gen_range(uint64_t seed, uint64_t p, uint32_t off, uint32_t len, uint8_t* out) {
+    const uint64_t key = mix64(seed ^ (p * 0xD1B54A32D192ED03ULL));
+    for (uint32_t i = 0; i < len;) {
+        const uint32_t b = off + i;
+        const uint64_t w = mix64(key + (uint64_t)(b / 8 + 1) * 0x9E3779B97F4A7C15ULL);
+        const uint32_t k = b % 8;
+        const uint32_t take = std::min<uint32_t>(8 - k, len - i);
+        std::memcpy(out + i, reinterpret_cast<const uint8_t*>(&w) + k, take);
+        i += take;
+    }
+}
+
+constexpr uint32_t kSubpiece = 16384;  // SUBPIECE_SIZE, piece_selector.rs:15
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 6) {
+        std::fprintf(stderr, "usage: %s expected.bin n piece_len last_len seed [peers] [subs/turn] [corrupt_every]\n",
+                     argv[0]);
+        return 2;
+    }
+    const char* exp_path = argv[1];
+    const uint32_t n = (uint32_t)std::strtoul(argv[2], nullptr, 10);
+    const uint32_t plen = (uint32_t)std::strtoul(argv[3], nullptr, 10);
+    const uint32_t last_len = (uint32_t)std::strtoul(argv[4], nullptr, 10);
+    const uint64_t seed = std::strtoull(argv[5], nullptr, 0);
+    const uint32_t peers = argc > 6 ? (uint32_t)std::atoi(argv[6]) : 32;
+    const uint32_t subs_per_turn = argc > 7 ? (uint32_t)std::atoi(argv[7]) : 4;
+    const uint32_t corrupt_every = argc > 8 ? (uint32_t)std::atoi(argv[8]) : 50;
+
+    std::vector<uint8_t> expected((size_t)n * 20);
+    FILE* f = std::fopen(exp_path, "rb");
+    if (!f || std::fread(expected.data(), 1, expected.size(), f) != expected.size()) {
+        std::fprintf(stderr, "cannot read %s\n", exp_path);
+        return 2;
+    }
+    std::fclose(f);
+
+    vx_config cfg;
+    vx_config_default(&cfg, plen);
+    cfg.slots = 4;
+    vx_ctx* ctx = nullptr;
+    if (int rc = vx_create(&cfg, &ctx)) {
+        std::fprintf(stderr, "vx_create: %d %s\n", rc, vx_last_error());
+        return 1;
+    }
+    // BufferPool: 256 buffers of piece_length (torrent.rs:344), one mmap.
+    const uint32_t nbuf = 256;
+    const size_t pool_bytes = (size_t)nbuf * plen;
+    uint8_t* pool = static_cast<uint8_t*>(
+        mmap(nullptr, pool_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_POPULATE, -1, 0));
+    if (pool == MAP_FAILED) return 1;
+    std::memset(pool, 0xEE, pool_bytes);  // stale bytes: never zeroed between uses
+    if (int rc = vx_register_host_buffer(ctx, pool, pool_bytes)) {
+        std::fprintf(stderr, "register: %d %s\n", rc, vx_last_error());
+        return 1;
+    }
+    std::vector<uint32_t> free_bufs;
+    for (uint32_t b = 0; b < nbuf; ++b) free_bufs.push_back(nbuf - 1 - b);
+
+    struct Download {
+        uint32_t piece, buf, next_sub, nsub, len;
+        bool corrupt;
+    };
+    std::deque<uint32_t> todo;
+    for (uint32_t i = 0; i < n; ++i) todo.push_back(i);
+    std::vector<Download> active;
+    std::vector<uint8_t> attempts(n, 0), complete(n, 0);
+    std::unordered_map<uint64_t, std::pair<uint32_t, double>> inflight;  // tag -> (buf, submit time)
+    std::vector<double> lat;
+    uint64_t tag_seq = 0, hashed = 0, rejected = 0, wrong = 0, turns = 0, bytes = 0;
+    std::vector<vx_completion> cq(512);
+    const double t0 = now_ms();
+    uint32_t done_count = 0;
+    while (done_count < n) {
+        ++turns;
+        // peers pick pieces (piece picker stand-in: next in order)
+        while (active.size() < peers && !todo.empty() && !free_bufs.empty()) {
+            const uint32_t p = todo.front();
+            todo.pop_front();
+            const uint32_t len = p == n - 1 ? last_len : plen;
+            const bool corrupt = corrupt_every && attempts[p] == 0 && p % corrupt_every == corrupt_every / 2;
+            active.push_back(Download{p, free_bufs.back(), 0, (len + kSubpiece - 1) / kSubpiece, len, corrupt});
+            free_bufs.pop_back();
+            attempts[p]++;
+        }
+        // receive: each active download gets subpieces (Piece::on_subpiece)
+        for (size_t a = 0; a < active.size();) {
+            Download& d = active[a];
+            for (uint32_t k = 0; k < subs_per_turn && d.next_sub < d.nsub; ++k, ++d.next_sub) {
+                const uint32_t off = d.next_sub * kSubpiece;
+                const uint32_t sl = std::min(kSubpiece, d.len - off);
+                uint8_t* dst = pool + (size_t)d.buf * plen + off;
+                gen_range(seed, d.piece, off, sl, dst);
+                if (d.corrupt && d.next_sub == d.nsub / 2) dst[sl / 3] ^= 0x40;
+            }
+            if (d.next_sub == d.nsub) {  // complete → hash (peer_connection.rs:1145)
+                const uint64_t tag = (tag_seq++ << 32) | d.piece;
+                const uint8_t* buf = pool + (size_t)d.buf * plen;
+                if (int rc = vx_submit(ctx, tag, buf, d.len, &expected[(size_t)d.piece * 20])) {
+                    std::fprintf(stderr, "vx_submit: %d %s\n", rc, vx_last_error());
+                    return 1;
+                }
+                inflight[tag] = {d.buf, now_ms()};
+                bytes += d.len;
+                active[a] = active.back();
+                active.pop_back();
+            } else {
+                ++a;
+            }
+        }
+        // end of loop turn: drain completions (event_loop.rs:554-557)
+        if (int rc = vx_flush(ctx)) {
+            std::fprintf(stderr, "vx_flush: %d\n", rc);
+            return 1;
+        }
+        for (;;) {
+            const int64_t k = vx_poll(ctx, cq.data(), cq.size());
+            if (k < 0) {
+                std::fprintf(stderr, "vx_poll: %lld %s\n", (long long)k, vx_last_error());
+                return 1;
+            }
+            for (int64_t j = 0; j < k; ++j) {
+                const vx_completion& c = cq[j];
+                const uint32_t p = (uint32_t)(c.tag & 0xFFFFFFFFu);
+                auto it = inflight.find(c.tag);
+                if (it == inflight.end()) return 1;
+                lat.push_back(now_ms() - it->second.second);
+                free_bufs.push_back(it->second.first);  // return_buffer
+                inflight.erase(it);
+                ++hashed;
+                const bool was_corrupt = corrupt_every && attempts[p] == 1 && p % corrupt_every == corrupt_every / 2;
+                if (c.matched) {
+                    if (was_corrupt) ++wrong;  // corrupted data must never verify
+                    complete[p] = 1;
+                    ++done_count;
+                } else {
+                    if (!was_corrupt) ++wrong;  // clean data must always verify
+                    ++rejected;
+                    todo.push_back(p);  // mark_not_downloaded → re-request
+                }
+            }
+            if ((size_t)k < cq.size()) break;
+        }
+        if (active.empty() && todo.empty() && !inflight.empty()) {
+            // nothing left to receive: block for the GPU like the loop's
+            // CQE wait would (torrent.rs:42, event_loop.rs:438-439)
+            vx_drain(ctx, 0);
+        }
+    }
+    const double el = now_ms() - t0;
+    vx_unregister_host_buffer(ctx, pool);
+    vx_destroy(ctx);
+    munmap(pool, pool_bytes);
+    std::sort(lat.begin(), lat.end());
+    auto pct = [&](double q) { return lat.empty() ? 0.0 : lat[std::min(lat.size() - 1, (size_t)(q * lat.size()))]; };
+    std::printf(
+        "{\"pieces\": %u, \"piece_len\": %u, \"hashed\": %llu, \"rejected\": %llu, \"wrong\": %llu, \"turns\": %llu, "
+        "\"elapsed_ms\": %.1f, \"GiBps\": %.3f, \"latency_ms_p50\": %.2f, \"latency_ms_p99\": %.2f, "
+        "\"latency_ms_max\": %.2f}\n",
+        n, plen, (unsigned long long)hashed, (unsigned long long)rejected, (unsigned long long)wrong,
+        (unsigned long long)turns, el, bytes / (el * 1e-3) / (1 << 30), pct(0.5), pct(0.99), lat.empty() ? 0 : lat.back());
+    return wrong == 0 && done_count == n ? 0 : 3;
+}

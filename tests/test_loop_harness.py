@@ -1,0 +1,33 @@
+"""GPU: vortex's download-path control flow (subpiece assembly into registered
+pool buffers → submit on completion → drain once per loop turn → re-request on
+mismatch) driven through the C ABI by tests/native/loop_harness.cpp."""
+import json
+import os
+import subprocess
+
+import pytest
+
+import oracle
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+THREADS = max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+@pytest.mark.parametrize("n,plen,last", [(600, 262144, 262144 - 16384 - 77), (97, 2097152, 1179648),
+                                         (2000, 32768, 164)])
+def test_download_loop(built, gpu, tmp_path, n, plen, last):
+    subprocess.run(["make", "-C", os.path.join(ROOT, "tests", "native"), "-s"], check=True)
+    seed = 0x5EED00AA
+    exp = oracle.pool_digest_synth(seed, 0, n, plen, last_index=n - 1, last_len=last, threads=THREADS)
+    p = tmp_path / "expected.bin"
+    p.write_bytes(exp)
+    out = subprocess.run([os.path.join(ROOT, "tests", "native", "loop_harness"), str(p), str(n), str(plen),
+                          str(last), hex(seed), "32", "4", "50"], capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    print(json.dumps(res))
+    corrupted = sum(1 for i in range(n) if i % 50 == 25)
+    assert res["wrong"] == 0
+    assert res["rejected"] == corrupted
+    assert res["hashed"] == n + corrupted

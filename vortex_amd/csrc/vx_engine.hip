@@ -75,6 +75,7 @@ struct DirectRun {
 struct Slot {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
+    hipEvent_t copied = nullptr;  // this slot's H2D finished on the copy stream
     uint64_t arena_cap = 0;
     uint32_t cap = 0;  // pieces
     uint8_t* d_arena = nullptr;
@@ -108,6 +109,13 @@ struct Slot {
 struct vx_ctx {
     vx_config cfg{};
     std::vector<Slot> slots;
+    // H2D copies are serialised across slots in launch order: each slot's
+    // stream first waits for the previous slot's copies (event), so PCIe
+    // moves one batch at a time at full rate and batch k's kernel starts as
+    // soon as its own bytes are in, while batch k+1 copies.  (Copies racing
+    // on all slot streams share PCIe and delay every kernel; one shared copy
+    // stream would head-of-line block behind kernels on the 4 HW queues.)
+    int last_launched = -1;
     int filling = -1;
     std::deque<vx_completion> done;
     std::map<uintptr_t, size_t> registered;
@@ -134,6 +142,7 @@ bool is_registered(const vx_ctx* c, const void* p, size_t len) {
 int free_slot_mem(Slot& s) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (s.done) (void)hipEventDestroy(s.done);
+    if (s.copied) (void)hipEventDestroy(s.copied);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     if (s.d_arena) (void)hipFree(s.d_arena);
     if (s.d_meta) (void)hipFree(s.d_meta);
@@ -148,6 +157,7 @@ int alloc_slot(Slot& s, uint64_t arena, uint32_t cap) {
     s.cap = cap;
     VX_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
     VX_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+    VX_HIP(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
     if (hipMalloc(&s.d_arena, arena) != hipSuccess) return fail(VX_ENOMEM, "device arena allocation failed");
     if (hipHostMalloc(&s.h_stage, arena, hipHostMallocDefault) != hipSuccess)
         return fail(VX_ENOMEM, "pinned stage allocation failed");
@@ -185,13 +195,21 @@ int launch_slot(vx_ctx* c, int si) {
         s.state = Slot::FREE;
         return 0;
     }
+    hipStream_t cs = s.stream;
+    if (c->last_launched >= 0 && c->last_launched != si)
+        VX_HIP(hipStreamWaitEvent(cs, c->slots[c->last_launched].copied, 0));
     for (const DirectRun& r : s.druns)
-        VX_HIP(hipMemcpyAsync(s.d_arena + r.lo, r.host, r.hi - r.lo, hipMemcpyHostToDevice, s.stream));
+        VX_HIP(hipMemcpyAsync(s.d_arena + r.lo, r.host, r.hi - r.lo, hipMemcpyHostToDevice, cs));
     for (const Run& r : s.runs)
-        VX_HIP(hipMemcpyAsync(s.d_arena + r.lo, s.h_stage + r.lo, r.hi - r.lo, hipMemcpyHostToDevice, s.stream));
+        VX_HIP(hipMemcpyAsync(s.d_arena + r.lo, s.h_stage + r.lo, r.hi - r.lo, hipMemcpyHostToDevice, cs));
     const uint32_t n = s.n;
-    if (s.has_expected)
-        VX_HIP(hipMemcpyAsync(s.d_expected, s.h_expected, (size_t)n * 20, hipMemcpyHostToDevice, s.stream));
+    if (s.has_expected) VX_HIP(hipMemcpyAsync(s.d_expected, s.h_expected, (size_t)n * 20, hipMemcpyHostToDevice, cs));
+    if (!s.uniform) {
+        VX_HIP(hipMemcpyAsync(s.d_offsets, s.h_offsets, (size_t)n * 8, hipMemcpyHostToDevice, cs));
+        VX_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)n * 4, hipMemcpyHostToDevice, cs));
+    }
+    VX_HIP(hipEventRecord(s.copied, cs));
+    c->last_launched = si;
     hipError_t e;
     if (s.uniform) {
         const uint32_t len = s.h_lens[0];
@@ -199,8 +217,6 @@ int launch_slot(vx_ctx* c, int si) {
         e = vx::launch_uniform(s.d_arena, stride, len, n, s.d_digests, s.has_expected ? s.d_expected : nullptr,
                                s.d_matched, s.stream, vx::kUniformDefault);
     } else {
-        VX_HIP(hipMemcpyAsync(s.d_offsets, s.h_offsets, (size_t)n * 8, hipMemcpyHostToDevice, s.stream));
-        VX_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)n * 4, hipMemcpyHostToDevice, s.stream));
         e = vx::launch_ragged(s.d_arena, s.d_offsets, s.d_lens, nullptr, n, s.d_digests,
                               s.has_expected ? s.d_expected : nullptr, s.d_matched, s.stream);
     }
