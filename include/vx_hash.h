@@ -114,6 +114,14 @@ int vx_unregister_host_buffer(vx_ctx* ctx, void* ptr);
  * slot is in flight, in which case it waits for the oldest batch (the
  * reference's spawn never refuses work either). */
 int vx_submit(vx_ctx* ctx, uint64_t tag, const uint8_t* data, uint32_t len, const uint8_t* expected);
+/* Device-resident expected-digest table: upload the
+ * torrent's `pieces` string (metadata.pieces, n_pieces x 20 B, the table the
+ * closure indexes at peer_connection.rs:1146) once; vx_submit_piece then
+ * names a row instead of passing 20 bytes per piece.  Replaces any previous
+ * table; requires no pieces in flight. */
+int vx_set_piece_table(vx_ctx* ctx, const uint8_t* table, uint32_t n_pieces);
+/* vx_submit with expected = row piece_index of the piece table. */
+int vx_submit_piece(vx_ctx* ctx, uint64_t tag, const uint8_t* data, uint32_t len, uint32_t piece_index);
 /* Launch whatever is queued (call once per event-loop turn, next to the
  * drain at event_loop.rs:554-557). */
 int vx_flush(vx_ctx* ctx);

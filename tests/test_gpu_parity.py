@@ -392,3 +392,30 @@ def test_verify_files_multi_file(built, gpu, tmp_path, golden):
     assert not all(got) and any(got)
     assert bad == sum(1 for i in range(n) if any(fi in (5, 7) and (fi == 7 or off + ln > (1 << 20))
                                                  for fi, off, ln in oracle.piece_segments(i, sizes, pl)))
+
+
+def test_piece_table_path(built, gpu, golden):
+    """§8f row 3: the torrent's `pieces` table uploaded once, pieces submitted
+    by index (vx_submit_piece), mixed with explicit-digest submits."""
+    from vortex_amd._lib import VxError
+    from vortex_amd.hash_pool import HashPool
+
+    n, pl = 300, 40000
+    pieces = [oracle.gen_piece(5, i, pl if i < n - 1 else 1234) for i in range(n)]
+    table = bytearray(b"".join(hashlib.sha1(p).digest() for p in pieces))
+    table[20 * 17] ^= 1  # row 17 is wrong: piece 17 must mismatch
+    with HashPool(pl, slots=3, batch_pieces=32) as pool:
+        with pytest.raises(VxError):
+            pool.spawn(0, 0, bytearray(pieces[0]), pl)  # no table yet
+        pool.set_piece_table(bytes(table))
+        for i, p in enumerate(pieces):
+            if i % 5 == 0:  # explicit digest interleaved
+                pool.spawn(i, 9, bytearray(p), len(p), hashlib.sha1(p).digest())
+            else:
+                pool.spawn(i, 9, bytearray(p), len(p))
+        pool.drain()
+        got = {r.index: (r.hash_matched, r.digest) for r in pool.try_iter()}
+    assert len(got) == n
+    for i, p in enumerate(pieces):
+        assert got[i][1] == hashlib.sha1(p).digest()
+        assert got[i][0] == (i != 17 or i % 5 == 0), i

@@ -30,7 +30,7 @@ VX_EBUSY = -16
 EXPORTS = (
     "vx_abi_version", "vx_last_error", "vx_strerror", "vx_device_count", "vx_config_default",
     "vx_create", "vx_destroy", "vx_register_host_buffer", "vx_unregister_host_buffer",
-    "vx_submit", "vx_flush", "vx_poll", "vx_drain", "vx_pending",
+    "vx_submit", "vx_flush", "vx_poll", "vx_drain", "vx_pending", "vx_set_piece_table", "vx_submit_piece",
     "vx_sha1_batch", "vx_verify_batch", "vx_verify_files",
     "vx_sha1_device_uniform", "vx_sha1_device_ragged", "vx_sort_order",
     "vx_synth_fill", "vx_sha1_device_uniform_variant", "vx_sha1_device_ragged_variant",
@@ -72,6 +72,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "vx_unregister_host_buffer": ([vp, vp], c.c_int),
         "vx_submit": ([vp, c.c_uint64, vp, c.c_uint32, vp], c.c_int),
         "vx_flush": ([vp], c.c_int),
+        "vx_set_piece_table": ([vp, vp, c.c_uint32], c.c_int),
+        "vx_submit_piece": ([vp, c.c_uint64, vp, c.c_uint32, c.c_uint32], c.c_int),
         "vx_poll": ([vp, c.POINTER(vx_completion), c.c_size_t], c.c_int64),
         "vx_drain": ([vp, c.c_uint32], c.c_int),
         "vx_pending": ([vp], c.c_uint64),

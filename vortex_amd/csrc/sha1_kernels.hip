@@ -84,7 +84,8 @@ __device__ __forceinline__ void hash_piece(State& s, const uint8_t* p, uint32_t 
 }
 
 __device__ __forceinline__ void emit(const State& s, uint32_t idx, uint8_t* __restrict__ digests,
-                                     const uint8_t* __restrict__ expected, uint8_t* __restrict__ matched) {
+                                     const uint8_t* __restrict__ expected, uint8_t* __restrict__ matched,
+                                     const uint32_t* __restrict__ exp_index = nullptr) {
     const uint32_t d0 = bswap(s.h0), d1 = bswap(s.h1), d2 = bswap(s.h2), d3 = bswap(s.h3), d4 = bswap(s.h4);
     if (digests) {
         uint32_t* o = reinterpret_cast<uint32_t*>(digests + (size_t)idx * 20);
@@ -95,7 +96,9 @@ __device__ __forceinline__ void emit(const State& s, uint32_t idx, uint8_t* __re
         o[4] = d4;
     }
     if (expected && matched) {
-        const uint32_t* x = reinterpret_cast<const uint32_t*>(expected + (size_t)idx * 20);
+        // exp_index: row of the device-resident piece table (vx_set_piece_table)
+        const uint32_t row = exp_index ? exp_index[idx] : idx;
+        const uint32_t* x = reinterpret_cast<const uint32_t*>(expected + (size_t)row * 20);
         const bool ok = (x[0] == d0) & (x[1] == d1) & (x[2] == d2) & (x[3] == d3) & (x[4] == d4);
         matched[idx] = ok ? 1 : 0;
     }
@@ -115,14 +118,15 @@ __global__ __launch_bounds__(kBlock) void sha1_uniform_kernel(const uint8_t* __r
                                                               uint32_t len, uint32_t n,
                                                               uint8_t* __restrict__ digests,
                                                               const uint8_t* __restrict__ expected,
-                                                              uint8_t* __restrict__ matched) {
+                                                              uint8_t* __restrict__ matched,
+                                                              const uint32_t* __restrict__ exp_index) {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     // Lanes past n re-hash piece n-1 (in bounds, wave stays convergent) and
     // store nothing.
     const uint32_t pi = kAlias ? 0 : (i < n ? i : n - 1);  // kAlias: diagnostic, every lane reads piece 0
     State s = iv();
     hash_piece<true, R>(s, base + (size_t)pi * stride, len, (len >> 7));
-    if (i < n) emit(s, i, digests, expected, matched);
+    if (i < n) emit(s, i, digests, expected, matched, exp_index);
 }
 
 __global__ __launch_bounds__(kBlock) void sha1_ragged_kernel(const uint8_t* __restrict__ base,
@@ -131,7 +135,8 @@ __global__ __launch_bounds__(kBlock) void sha1_ragged_kernel(const uint8_t* __re
                                                              const uint32_t* __restrict__ order, uint32_t n,
                                                              uint8_t* __restrict__ digests,
                                                              const uint8_t* __restrict__ expected,
-                                                             uint8_t* __restrict__ matched) {
+                                                             uint8_t* __restrict__ matched,
+                                                             const uint32_t* __restrict__ exp_index) {
     const uint32_t j = blockIdx.x * kBlock + threadIdx.x;
     const uint32_t jj = j < n ? j : n - 1;
     const uint32_t idx = order ? order[jj] : jj;
@@ -140,7 +145,7 @@ __global__ __launch_bounds__(kBlock) void sha1_ragged_kernel(const uint8_t* __re
     const uint32_t ng_wave = __builtin_amdgcn_readfirstlane(wave_max(len >> 7));
     State s = iv();
     hash_piece<false>(s, p, len, ng_wave);
-    if (j < n) emit(s, idx, digests, expected, matched);
+    if (j < n) emit(s, idx, digests, expected, matched, exp_index);
 }
 
 
@@ -254,7 +259,8 @@ __global__ __launch_bounds__(kPairBlock) void sha1_split_kernel(const uint8_t* _
                                                                 uint32_t len, uint32_t n,
                                                                 uint8_t* __restrict__ digests,
                                                                 const uint8_t* __restrict__ expected,
-                                                                uint8_t* __restrict__ matched) {
+                                                                uint8_t* __restrict__ matched,
+                                                                const uint32_t* __restrict__ exp_index) {
     __shared__ SplitLds lds;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -336,15 +342,16 @@ __global__ __launch_bounds__(kPairBlock) void sha1_split_kernel(const uint8_t* _
             rounds_lds(s, lds.w[b & 1], lane);
             __syncthreads();
         }
-        if (i < n) emit(s, i, digests, expected, matched);
+        if (i < n) emit(s, i, digests, expected, matched, exp_index);
     }
 }
 
 hipError_t launch_uniform_split(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
-                                const uint8_t* expected, uint8_t* matched, hipStream_t stream) {
+                                const uint8_t* expected, uint8_t* matched, hipStream_t stream,
+                                const uint32_t* exp_index) {
     const uint32_t blocks = (n + 63) / 64;
     hipLaunchKernelGGL(sha1_split_kernel, dim3(blocks), dim3(kPairBlock), 0, stream, base, stride, len, n, digests,
-                       expected, matched);
+                       expected, matched, exp_index);
     return hipGetLastError();
 }
 
@@ -389,7 +396,7 @@ __device__ __forceinline__ void pad_words(uint32_t (&w)[16], const uint8_t* q, u
 __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lens,
     const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ digests,
-    const uint8_t* __restrict__ expected, uint8_t* __restrict__ matched) {
+    const uint8_t* __restrict__ expected, uint8_t* __restrict__ matched, const uint32_t* __restrict__ exp_index) {
     __shared__ SplitLds lds;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -445,39 +452,41 @@ __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
             if (b < nb) s = t;
             __syncthreads();
         }
-        if (j < n) emit(s, idx, digests, expected, matched);
+        if (j < n) emit(s, idx, digests, expected, matched, exp_index);
     }
 }
 
 hipError_t launch_ragged_split(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens,
                                const uint32_t* order, uint32_t n, uint8_t* digests, const uint8_t* expected,
-                               uint8_t* matched, hipStream_t stream) {
+                               uint8_t* matched, hipStream_t stream, const uint32_t* exp_index) {
     const uint32_t blocks = (n + 63) / 64;
     hipLaunchKernelGGL(sha1_ragged_split_kernel, dim3(blocks), dim3(kPairBlock), 0, stream, base, offsets, lens,
-                       order, n, digests, expected, matched);
+                       order, n, digests, expected, matched, exp_index);
     return hipGetLastError();
 }
 
 template <int R, bool kAlias = false>
 hipError_t launch_uniform_lane_r(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
-                                 const uint8_t* expected, uint8_t* matched, hipStream_t stream) {
+                                 const uint8_t* expected, uint8_t* matched, hipStream_t stream,
+                                 const uint32_t* exp_index) {
     const uint32_t blocks = (n + kBlock - 1) / kBlock;
     hipLaunchKernelGGL((sha1_uniform_kernel<R, kAlias>), dim3(blocks), dim3(kBlock), 0, stream, base, stride, len, n, digests,
-                       expected, matched);
+                       expected, matched, exp_index);
     return hipGetLastError();
 }
 
 hipError_t launch_uniform_lane(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
-                               const uint8_t* expected, uint8_t* matched, hipStream_t stream) {
-    return launch_uniform_lane_r<kRing>(base, stride, len, n, digests, expected, matched, stream);
+                               const uint8_t* expected, uint8_t* matched, hipStream_t stream,
+                               const uint32_t* exp_index) {
+    return launch_uniform_lane_r<kRing>(base, stride, len, n, digests, expected, matched, stream, exp_index);
 }
 
 hipError_t launch_ragged_lane(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens,
                               const uint32_t* order, uint32_t n, uint8_t* digests, const uint8_t* expected,
-                              uint8_t* matched, hipStream_t stream) {
+                              uint8_t* matched, hipStream_t stream, const uint32_t* exp_index) {
     const uint32_t blocks = (n + kBlock - 1) / kBlock;
     hipLaunchKernelGGL(sha1_ragged_kernel, dim3(blocks), dim3(kBlock), 0, stream, base, offsets, lens, order, n,
-                       digests, expected, matched);
+                       digests, expected, matched, exp_index);
     return hipGetLastError();
 }
 
@@ -485,28 +494,29 @@ hipError_t launch_ragged_lane(const uint8_t* base, const uint64_t* offsets, cons
 
 namespace vx {
 hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
-                          const uint8_t* expected, uint8_t* matched, hipStream_t stream, int variant) {
-    if (variant == kUniformLane) return launch_uniform_lane(base, stride, len, n, digests, expected, matched, stream);
-    if (variant == kUniformSplit) return launch_uniform_split(base, stride, len, n, digests, expected, matched, stream);
+                          const uint8_t* expected, uint8_t* matched, hipStream_t stream, int variant,
+                          const uint32_t* exp_index) {
+    if (variant == kUniformLane) return launch_uniform_lane(base, stride, len, n, digests, expected, matched, stream, exp_index);
+    if (variant == kUniformSplit) return launch_uniform_split(base, stride, len, n, digests, expected, matched, stream, exp_index);
     // Default: the integer VALU is the roofline once every SIMD has a wave
     // (n >= 65,536 with the lane kernel), and the split kernel's extra LDS
     // hand-off only costs there.  Below kSplitMaxPieces the chip has idle
     // SIMDs and the split kernel's shorter per-wave chain (405 vs 613 VALU per
     // block) finishes each piece sooner (DESIGN.md "Kernels", measured).
-    if (n <= kSplitMaxPieces) return launch_uniform_split(base, stride, len, n, digests, expected, matched, stream);
-    return launch_uniform_lane(base, stride, len, n, digests, expected, matched, stream);
+    if (n <= kSplitMaxPieces) return launch_uniform_split(base, stride, len, n, digests, expected, matched, stream, exp_index);
+    return launch_uniform_lane(base, stride, len, n, digests, expected, matched, stream, exp_index);
 }
 }  // namespace vx
 
 namespace vx {
 hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens, const uint32_t* order,
                          uint32_t n, uint8_t* digests, const uint8_t* expected, uint8_t* matched,
-                         hipStream_t stream, int variant) {
-    if (variant == kUniformLane) return launch_ragged_lane(base, offsets, lens, order, n, digests, expected, matched, stream);
+                         hipStream_t stream, int variant, const uint32_t* exp_index) {
+    if (variant == kUniformLane) return launch_ragged_lane(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
     if (variant == kUniformSplit)
-        return launch_ragged_split(base, offsets, lens, order, n, digests, expected, matched, stream);
+        return launch_ragged_split(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
     if (n <= kSplitMaxPieces)
-        return launch_ragged_split(base, offsets, lens, order, n, digests, expected, matched, stream);
-    return launch_ragged_lane(base, offsets, lens, order, n, digests, expected, matched, stream);
+        return launch_ragged_split(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
+    return launch_ragged_lane(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
 }
 }  // namespace vx

@@ -88,6 +88,8 @@ struct Slot {
     uint8_t* h_expected = nullptr;
     uint8_t* h_digests = nullptr;
     uint8_t* h_matched = nullptr;
+    uint32_t* h_pidx = nullptr;  // piece-table rows (vx_submit_piece)
+    uint32_t* d_pidx = nullptr;
     uint64_t* d_offsets = nullptr;
     uint32_t* d_lens = nullptr;
     uint8_t* d_expected = nullptr;
@@ -100,6 +102,7 @@ struct Slot {
     uint64_t bytes = 0;
     bool uniform = true;
     bool has_expected = false;
+    bool use_table = false;  // expected digests come from the device piece table
     enum State { FREE, FILLING, INFLIGHT } state = FREE;
     uint64_t seq = 0;
 };
@@ -116,6 +119,9 @@ struct vx_ctx {
     // on all slot streams share PCIe and delay every kernel; one shared copy
     // stream would head-of-line block behind kernels on the 4 HW queues.)
     int last_launched = -1;
+    // Device-resident `pieces` table (vx_set_piece_table).
+    uint8_t* d_table = nullptr;
+    uint32_t n_table = 0;
     int filling = -1;
     std::deque<vx_completion> done;
     std::map<uintptr_t, size_t> registered;
@@ -161,19 +167,22 @@ int alloc_slot(Slot& s, uint64_t arena, uint32_t cap) {
     if (hipMalloc(&s.d_arena, arena) != hipSuccess) return fail(VX_ENOMEM, "device arena allocation failed");
     if (hipHostMalloc(&s.h_stage, arena, hipHostMallocDefault) != hipSuccess)
         return fail(VX_ENOMEM, "pinned stage allocation failed");
-    const size_t meta = (size_t)cap * (8 + 4 + 20 + 20 + 1) + 64;
+    const size_t meta = (size_t)cap * (8 + 4 + 4 + 20 + 20 + 1) + 64;
     if (hipHostMalloc(&s.h_meta, meta, hipHostMallocDefault) != hipSuccess)
         return fail(VX_ENOMEM, "pinned metadata allocation failed");
     if (hipMalloc(&s.d_meta, meta) != hipSuccess) return fail(VX_ENOMEM, "device metadata allocation failed");
-    auto carve = [cap](uint8_t* b, uint64_t*& off, uint32_t*& lens, uint8_t*& exp, uint8_t*& dig, uint8_t*& m) {
+    // offsets | lens | piece rows | expected | digests | verdicts (all 4-byte aligned)
+    auto carve = [cap](uint8_t* b, uint64_t*& off, uint32_t*& lens, uint32_t*& pidx, uint8_t*& exp, uint8_t*& dig,
+                       uint8_t*& m) {
         off = reinterpret_cast<uint64_t*>(b);
         lens = reinterpret_cast<uint32_t*>(b + (size_t)cap * 8);
-        exp = b + (size_t)cap * 12;
-        dig = b + (size_t)cap * 32;
-        m = b + (size_t)cap * 52;
+        pidx = reinterpret_cast<uint32_t*>(b + (size_t)cap * 12);
+        exp = b + (size_t)cap * 16;
+        dig = b + (size_t)cap * 36;
+        m = b + (size_t)cap * 56;
     };
-    carve(s.h_meta, s.h_offsets, s.h_lens, s.h_expected, s.h_digests, s.h_matched);
-    carve(s.d_meta, s.d_offsets, s.d_lens, s.d_expected, s.d_digests, s.d_matched);
+    carve(s.h_meta, s.h_offsets, s.h_lens, s.h_pidx, s.h_expected, s.h_digests, s.h_matched);
+    carve(s.d_meta, s.d_offsets, s.d_lens, s.d_pidx, s.d_expected, s.d_digests, s.d_matched);
     s.tags.reserve(cap);
     return 0;
 }
@@ -186,6 +195,7 @@ void reset_fill(Slot& s) {
     s.bytes = 0;
     s.uniform = true;
     s.has_expected = false;
+    s.use_table = false;
 }
 
 int launch_slot(vx_ctx* c, int si) {
@@ -203,7 +213,12 @@ int launch_slot(vx_ctx* c, int si) {
     for (const Run& r : s.runs)
         VX_HIP(hipMemcpyAsync(s.d_arena + r.lo, s.h_stage + r.lo, r.hi - r.lo, hipMemcpyHostToDevice, cs));
     const uint32_t n = s.n;
-    if (s.has_expected) VX_HIP(hipMemcpyAsync(s.d_expected, s.h_expected, (size_t)n * 20, hipMemcpyHostToDevice, cs));
+    if (s.use_table)
+        VX_HIP(hipMemcpyAsync(s.d_pidx, s.h_pidx, (size_t)n * 4, hipMemcpyHostToDevice, cs));
+    else if (s.has_expected)
+        VX_HIP(hipMemcpyAsync(s.d_expected, s.h_expected, (size_t)n * 20, hipMemcpyHostToDevice, cs));
+    const uint8_t* d_exp = s.use_table ? c->d_table : (s.has_expected ? s.d_expected : nullptr);
+    const uint32_t* d_row = s.use_table ? s.d_pidx : nullptr;
     if (!s.uniform) {
         VX_HIP(hipMemcpyAsync(s.d_offsets, s.h_offsets, (size_t)n * 8, hipMemcpyHostToDevice, cs));
         VX_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)n * 4, hipMemcpyHostToDevice, cs));
@@ -214,11 +229,11 @@ int launch_slot(vx_ctx* c, int si) {
     if (s.uniform) {
         const uint32_t len = s.h_lens[0];
         const uint64_t stride = align_up(std::max<uint32_t>(len, 1), kAlign);
-        e = vx::launch_uniform(s.d_arena, stride, len, n, s.d_digests, s.has_expected ? s.d_expected : nullptr,
-                               s.d_matched, s.stream, vx::kUniformDefault);
+        e = vx::launch_uniform(s.d_arena, stride, len, n, s.d_digests, d_exp, s.d_matched, s.stream,
+                               vx::kUniformDefault, d_row);
     } else {
-        e = vx::launch_ragged(s.d_arena, s.d_offsets, s.d_lens, nullptr, n, s.d_digests,
-                              s.has_expected ? s.d_expected : nullptr, s.d_matched, s.stream);
+        e = vx::launch_ragged(s.d_arena, s.d_offsets, s.d_lens, nullptr, n, s.d_digests, d_exp, s.d_matched,
+                              s.stream, vx::kUniformDefault, d_row);
     }
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
     VX_HIP(hipMemcpyAsync(s.h_digests, s.d_digests, (size_t)n * 20, hipMemcpyDeviceToHost, s.stream));
@@ -279,15 +294,20 @@ int acquire_filling(vx_ctx* c) {
     }
 }
 
-int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, const uint8_t* expected) {
+// piece_row < 0: compare with `expected` (may be NULL); piece_row >= 0:
+// compare with row piece_row of the device piece table.
+int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, const uint8_t* expected,
+                int64_t piece_row = -1) {
     if (c->sticky) return c->sticky;
     if (!data && len) return fail(VX_EINVAL, "vx_submit: data is NULL");
     if (len > c->cfg.max_piece_len) return fail(VX_ERANGE, "vx_submit: piece longer than max_piece_len");
+    const bool table = piece_row >= 0;
     int si = acquire_filling(c);
     if (si < 0) return si;
     Slot* s = &c->slots[si];
     uint64_t off = align_up(s->bytes, kAlign);
-    if (s->n == s->cap || off + len > s->arena_cap) {
+    // a slot holds either table-indexed or explicit-digest pieces
+    if (s->n == s->cap || off + len > s->arena_cap || (s->n && s->use_table != table)) {
         int rc = launch_slot(c, si);
         if (rc) return rc;
         si = acquire_filling(c);
@@ -320,7 +340,11 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
     // Equal lengths at 256-byte aligned back-to-back offsets are a uniform
     // batch: offset(i) = i * align_up(len, 256) (the uniform kernel's layout).
     if (i > 0 && len != s->h_lens[0]) s->uniform = false;
-    if (expected) {
+    if (table) {
+        s->h_pidx[i] = (uint32_t)piece_row;
+        s->use_table = true;
+        s->has_expected = true;
+    } else if (expected) {
         std::memcpy(s->h_expected + (size_t)i * 20, expected, 20);
         if (i > 0 && !s->has_expected) {
             // earlier pieces of this batch had no expected digest: they get
@@ -409,6 +433,7 @@ int vx_destroy(vx_ctx* c) {
     set_device(c);
     for (auto& r : c->registered) (void)hipHostUnregister(reinterpret_cast<void*>(r.first));
     for (auto& s : c->slots) free_slot_mem(s);
+    if (c->d_table) (void)hipFree(c->d_table);
     delete c;
     return rc;
 }
@@ -446,6 +471,30 @@ int vx_submit(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, const 
     int rc = set_device(c);
     if (rc) return rc;
     return submit_impl(c, tag, data, len, expected);
+}
+
+int vx_set_piece_table(vx_ctx* c, const uint8_t* table, uint32_t n_pieces) {
+    if (!c || (n_pieces && !table)) return fail(VX_EINVAL, "vx_set_piece_table: bad argument");
+    if (c->pending || c->filling >= 0) return fail(VX_EBUSY, "vx_set_piece_table: pieces in flight");
+    int rc = set_device(c);
+    if (rc) return rc;
+    if (c->d_table) (void)hipFree(c->d_table);
+    c->d_table = nullptr;
+    c->n_table = 0;
+    if (!n_pieces) return 0;
+    if (hipMalloc(&c->d_table, (size_t)n_pieces * 20) != hipSuccess)
+        return fail(VX_ENOMEM, "vx_set_piece_table: device allocation failed");
+    VX_HIP(hipMemcpy(c->d_table, table, (size_t)n_pieces * 20, hipMemcpyHostToDevice));
+    c->n_table = n_pieces;
+    return 0;
+}
+
+int vx_submit_piece(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, uint32_t piece_index) {
+    if (!c) return fail(VX_EINVAL, "vx_submit_piece: NULL context");
+    if (piece_index >= c->n_table) return fail(VX_EINVAL, "vx_submit_piece: piece_index outside the piece table");
+    int rc = set_device(c);
+    if (rc) return rc;
+    return submit_impl(c, tag, data, len, nullptr, (int64_t)piece_index);
 }
 
 int vx_flush(vx_ctx* c) {

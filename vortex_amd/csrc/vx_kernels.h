@@ -16,21 +16,25 @@ enum UniformVariant { kUniformDefault = 0, kUniformLane = 1, kUniformSplit = 2 }
 constexpr uint32_t kSplitMaxPieces = 16384;  // default picks split at or below this batch size
 
 hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
-                          const uint8_t* expected, uint8_t* matched, hipStream_t stream, int variant = 0);
+                          const uint8_t* expected, uint8_t* matched, hipStream_t stream, int variant = 0,
+                          const uint32_t* exp_index = nullptr);
 hipError_t launch_uniform_lane(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
-                               const uint8_t* expected, uint8_t* matched, hipStream_t stream);
+                               const uint8_t* expected, uint8_t* matched, hipStream_t stream,
+                               const uint32_t* exp_index = nullptr);
 hipError_t launch_uniform_split(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
-                                const uint8_t* expected, uint8_t* matched, hipStream_t stream);
+                                const uint8_t* expected, uint8_t* matched, hipStream_t stream,
+                                const uint32_t* exp_index = nullptr);
 
 hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens, const uint32_t* order,
                          uint32_t n, uint8_t* digests, const uint8_t* expected, uint8_t* matched,
-                         hipStream_t stream, int variant = 0);
+                         hipStream_t stream, int variant = 0,
+                          const uint32_t* exp_index = nullptr);
 hipError_t launch_ragged_lane(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens,
                               const uint32_t* order, uint32_t n, uint8_t* digests, const uint8_t* expected,
-                              uint8_t* matched, hipStream_t stream);
+                              uint8_t* matched, hipStream_t stream, const uint32_t* exp_index = nullptr);
 hipError_t launch_ragged_split(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens,
                                const uint32_t* order, uint32_t n, uint8_t* digests, const uint8_t* expected,
-                               uint8_t* matched, hipStream_t stream);
+                               uint8_t* matched, hipStream_t stream, const uint32_t* exp_index = nullptr);
 
 hipError_t launch_synth_fill(uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint64_t first,
                              uint64_t seed, uint32_t corrupt_every, hipStream_t stream);

@@ -126,19 +126,31 @@ class HashPool:
         self._registered.pop(addr, None)
 
     # -- download path -------------------------------------------------------
-    def spawn(self, index: int, conn_id: int, buffer, piece_len: int, expected_hash: bytes) -> None:
+    def spawn(self, index: int, conn_id: int, buffer, piece_len: int, expected_hash: Optional[bytes] = None) -> None:
         """peer_connection.rs:1145-1158: hash buffer[:piece_len] against
-        expected_hash; the result comes back from try_recv()."""
-        if len(expected_hash) != 20:
+        expected_hash (or, when None, against row `index` of the table given
+        to set_piece_table); the result comes back from try_recv()."""
+        if expected_hash is not None and len(expected_hash) != 20:
             raise ValueError("expected_hash must be 20 bytes")
         addr, keep = _addr_of(buffer)
         if piece_len > memoryview(buffer).nbytes:
             raise ValueError("piece_len exceeds buffer size")
         tag = self._next_tag
         self._next_tag += 1
-        exp = ctypes.create_string_buffer(bytes(expected_hash), 20)
-        check(lib().vx_submit(self._h, tag, addr, piece_len, exp), "vx_submit")
+        if expected_hash is None:
+            check(lib().vx_submit_piece(self._h, tag, addr, piece_len, index), "vx_submit_piece")
+        else:
+            exp = ctypes.create_string_buffer(bytes(expected_hash), 20)
+            check(lib().vx_submit(self._h, tag, addr, piece_len, exp), "vx_submit")
         self._inflight[tag] = (index, conn_id, buffer, keep)
+
+    def set_piece_table(self, pieces: bytes) -> None:
+        """Upload the torrent's `pieces` string (n x 20 B) once; afterwards
+        spawn(..., expected_hash=None) compares on the device by index."""
+        if len(pieces) % 20:
+            raise ValueError("pieces table must be a multiple of 20 bytes")
+        buf = ctypes.create_string_buffer(bytes(pieces), max(1, len(pieces)))
+        check(lib().vx_set_piece_table(self._h, buf, len(pieces) // 20), "vx_set_piece_table")
 
     def flush(self) -> None:
         """Launch everything queued; call once per event-loop turn."""
