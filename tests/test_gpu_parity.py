@@ -419,3 +419,42 @@ def test_piece_table_path(built, gpu, golden):
     for i, p in enumerate(pieces):
         assert got[i][1] == hashlib.sha1(p).digest()
         assert got[i][0] == (i != 17 or i % 5 == 0), i
+
+
+@pytest.mark.parametrize("pl,slot_mib,batch", [(1 << 20, 64, 256), (2 * 1024 * 1024 + 16384, 3, 3),
+                                               (4 << 20, 16, 5)])
+def test_verify_files_chunked(built, gpu, tmp_path, pl, slot_mib, batch):
+    """Pieces > 256 KiB take the resumable chunked path:
+    multi-file layout, short last piece, a flipped byte, a truncated file and a
+    missing file; small slots force several windows."""
+    from vortex_amd.hash_pool import HashPool
+
+    sizes = [7, 3 * pl + 12345, 0, pl // 2 + 1, 5 * pl, 64, 2 * pl - 100]
+    paths = []
+    for k, L in enumerate(sizes):
+        p = tmp_path / f"c{k}.bin"
+        p.write_bytes(oracle.gen_piece(11, k, L))
+        paths.append(str(p))
+    data = b"".join(open(p, "rb").read() for p in paths)
+    exp = b"".join(hashlib.sha1(data[i:i + pl]).digest() for i in range(0, len(data), pl))
+    n = len(exp) // 20
+    with HashPool(pl, slots=3, batch_pieces=batch, slot_bytes=slot_mib << 20) as pool:
+        got, bad = pool.verify_files(paths, sizes, pl, exp, io_threads=5)
+        assert got == [True] * n and bad == 0
+        with open(paths[4], "r+b") as f:  # flip one byte deep inside file 4
+            f.seek(3 * pl + 999)
+            b = f.read(1)
+            f.seek(3 * pl + 999)
+            f.write(bytes([b[0] ^ 1]))
+        with open(paths[1], "r+b") as f:
+            f.truncate(2 * pl)
+        os.unlink(paths[6])
+        got, bad = pool.verify_files(paths, sizes, pl, exp, io_threads=5)
+        # the async path still works afterwards on the same context
+        pool.spawn(0, 0, bytearray(data[:pl]), pl, exp[:20])
+        pool.drain()
+        r = pool.try_recv()
+        assert r.index == 0 and r.hash_matched
+    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
+    assert got == want
+    assert not all(got) and any(got)

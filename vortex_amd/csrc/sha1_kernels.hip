@@ -393,10 +393,20 @@ __device__ __forceinline__ void pad_words(uint32_t (&w)[16], const uint8_t* q, u
     }
 }
 
+// kChunked: resumable hashing of one chunk per lane.  SHA-1's
+// chaining state is 20 bytes, so a piece can be compressed chunk by chunk
+// across launches: lane j hashes bytes [poffs[j], poffs[j]+lens[j]) of piece
+// pids[j] (total length tlens[j]) starting from states[pid] (or the IV when
+// poffs[j] == 0); a chunk that ends the piece pads with the piece's total
+// length and emits digest/verdict for row pid, any other chunk (a multiple of
+// 64 bytes) stores the state back.
+template <bool kChunked>
 __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lens,
     const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ digests,
-    const uint8_t* __restrict__ expected, uint8_t* __restrict__ matched, const uint32_t* __restrict__ exp_index) {
+    const uint8_t* __restrict__ expected, uint8_t* __restrict__ matched, const uint32_t* __restrict__ exp_index,
+    const uint32_t* __restrict__ pids, const uint64_t* __restrict__ poffs, const uint64_t* __restrict__ tlens,
+    uint32_t* __restrict__ states) {
     __shared__ SplitLds lds;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -405,9 +415,13 @@ __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
     const uint32_t idx = order ? order[jj] : jj;
     const uint32_t len = lens[idx];
     const uint8_t* p = base + offsets[idx];
+    const uint32_t pid = kChunked ? pids[idx] : idx;
+    const uint64_t poff = kChunked ? poffs[idx] : 0;
+    const uint64_t tlen = kChunked ? tlens[idx] : len;
+    const bool final_chunk = poff + len == tlen;
     const uint32_t nfull = len >> 6;
     const uint32_t rem = len & 63u;
-    const uint32_t nb = nfull + (rem <= 55 ? 1u : 2u);
+    const uint32_t nb = final_chunk ? nfull + (rem <= 55 ? 1u : 2u) : nfull;
     const uint32_t nb_wave = __builtin_amdgcn_readfirstlane(wave_max(nb));
 
     if (wave == 1) {
@@ -434,7 +448,8 @@ __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
                     if (b < nfull) {
                         le_words(w, ring[r][0], ring[r][1], ring[r][2], ring[r][3]);
                     } else {
-                        pad_words(w, q, rem, len, b - nfull);
+                        // padding blocks (final chunks; other lanes are idle here)
+                        pad_words(w, q, rem, tlen, b - nfull);
                     }
                     expand_store(w, lds.w[b & 1], lane);
                     __syncthreads();
@@ -445,6 +460,10 @@ __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
     } else {
         // ---------------- consumer ----------------
         State s = iv();
+        if (kChunked && poff != 0) {
+            const uint32_t* st = states + (size_t)pid * 5;
+            s = State{st[0], st[1], st[2], st[3], st[4]};
+        }
         __syncthreads();
         for (uint32_t b = 0; b < nb_wave; ++b) {
             State t = s;
@@ -452,7 +471,18 @@ __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
             if (b < nb) s = t;
             __syncthreads();
         }
-        if (j < n) emit(s, idx, digests, expected, matched, exp_index);
+        if (j < n) {
+            if (!kChunked || final_chunk) {
+                emit(s, pid, digests, expected, matched, exp_index);
+            } else {
+                uint32_t* st = states + (size_t)pid * 5;
+                st[0] = s.h0;
+                st[1] = s.h1;
+                st[2] = s.h2;
+                st[3] = s.h3;
+                st[4] = s.h4;
+            }
+        }
     }
 }
 
@@ -460,8 +490,18 @@ hipError_t launch_ragged_split(const uint8_t* base, const uint64_t* offsets, con
                                const uint32_t* order, uint32_t n, uint8_t* digests, const uint8_t* expected,
                                uint8_t* matched, hipStream_t stream, const uint32_t* exp_index) {
     const uint32_t blocks = (n + 63) / 64;
-    hipLaunchKernelGGL(sha1_ragged_split_kernel, dim3(blocks), dim3(kPairBlock), 0, stream, base, offsets, lens,
-                       order, n, digests, expected, matched, exp_index);
+    hipLaunchKernelGGL(sha1_ragged_split_kernel<false>, dim3(blocks), dim3(kPairBlock), 0, stream, base, offsets,
+                       lens, order, n, digests, expected, matched, exp_index, nullptr, nullptr, nullptr, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_chunk(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens, uint32_t n,
+                        const uint32_t* pids, const uint64_t* poffs, const uint64_t* tlens, uint32_t* states,
+                        uint8_t* digests, const uint8_t* expected, uint8_t* matched, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const uint32_t blocks = (n + 63) / 64;
+    hipLaunchKernelGGL(sha1_ragged_split_kernel<true>, dim3(blocks), dim3(kPairBlock), 0, stream, base, offsets,
+                       lens, nullptr, n, digests, expected, matched, nullptr, pids, poffs, tlens, states);
     return hipGetLastError();
 }
 

@@ -88,8 +88,12 @@ struct Slot {
     uint8_t* h_expected = nullptr;
     uint8_t* h_digests = nullptr;
     uint8_t* h_matched = nullptr;
-    uint32_t* h_pidx = nullptr;  // piece-table rows (vx_submit_piece)
+    uint32_t* h_pidx = nullptr;  // piece-table rows (vx_submit_piece) / piece ids (chunks)
     uint32_t* d_pidx = nullptr;
+    uint64_t* h_poff = nullptr;  // chunked re-verify: chunk offset within its piece
+    uint64_t* d_poff = nullptr;
+    uint64_t* h_tlen = nullptr;  // chunked re-verify: the piece's total length
+    uint64_t* d_tlen = nullptr;
     uint64_t* d_offsets = nullptr;
     uint32_t* d_lens = nullptr;
     uint8_t* d_expected = nullptr;
@@ -167,22 +171,24 @@ int alloc_slot(Slot& s, uint64_t arena, uint32_t cap) {
     if (hipMalloc(&s.d_arena, arena) != hipSuccess) return fail(VX_ENOMEM, "device arena allocation failed");
     if (hipHostMalloc(&s.h_stage, arena, hipHostMallocDefault) != hipSuccess)
         return fail(VX_ENOMEM, "pinned stage allocation failed");
-    const size_t meta = (size_t)cap * (8 + 4 + 4 + 20 + 20 + 1) + 64;
+    const size_t meta = (size_t)cap * (8 + 4 + 4 + 20 + 20 + 8 + 8 + 1) + 64;
     if (hipHostMalloc(&s.h_meta, meta, hipHostMallocDefault) != hipSuccess)
         return fail(VX_ENOMEM, "pinned metadata allocation failed");
     if (hipMalloc(&s.d_meta, meta) != hipSuccess) return fail(VX_ENOMEM, "device metadata allocation failed");
-    // offsets | lens | piece rows | expected | digests | verdicts (all 4-byte aligned)
-    auto carve = [cap](uint8_t* b, uint64_t*& off, uint32_t*& lens, uint32_t*& pidx, uint8_t*& exp, uint8_t*& dig,
-                       uint8_t*& m) {
+    // offsets | chunk offsets | total lens | lens | piece rows | expected | digests | verdicts
+    auto carve = [cap](uint8_t* b, uint64_t*& off, uint64_t*& poff, uint64_t*& tlen, uint32_t*& lens,
+                       uint32_t*& pidx, uint8_t*& exp, uint8_t*& dig, uint8_t*& m) {
         off = reinterpret_cast<uint64_t*>(b);
-        lens = reinterpret_cast<uint32_t*>(b + (size_t)cap * 8);
-        pidx = reinterpret_cast<uint32_t*>(b + (size_t)cap * 12);
-        exp = b + (size_t)cap * 16;
-        dig = b + (size_t)cap * 36;
-        m = b + (size_t)cap * 56;
+        poff = reinterpret_cast<uint64_t*>(b + (size_t)cap * 8);
+        tlen = reinterpret_cast<uint64_t*>(b + (size_t)cap * 16);
+        lens = reinterpret_cast<uint32_t*>(b + (size_t)cap * 24);
+        pidx = reinterpret_cast<uint32_t*>(b + (size_t)cap * 28);
+        exp = b + (size_t)cap * 32;
+        dig = b + (size_t)cap * 52;
+        m = b + (size_t)cap * 72;
     };
-    carve(s.h_meta, s.h_offsets, s.h_lens, s.h_pidx, s.h_expected, s.h_digests, s.h_matched);
-    carve(s.d_meta, s.d_offsets, s.d_lens, s.d_pidx, s.d_expected, s.d_digests, s.d_matched);
+    carve(s.h_meta, s.h_offsets, s.h_poff, s.h_tlen, s.h_lens, s.h_pidx, s.h_expected, s.h_digests, s.h_matched);
+    carve(s.d_meta, s.d_offsets, s.d_poff, s.d_tlen, s.d_lens, s.d_pidx, s.d_expected, s.d_digests, s.d_matched);
     s.tags.reserve(cap);
     return 0;
 }
@@ -590,11 +596,203 @@ int vx_verify_batch(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens,
 }
 
 
-// Bulk re-verify from disk (include/vx_hash.h).  The reader threads pread
-// each slot's pieces straight into that slot's pinned stage (segments back
-// to back, file_store.rs:240-298 byte ranges), then the slot launches
-// (one H2D run, kernel, D2H verdicts) while the next free slot is read.
-// Completions are consumed here; they never reach vx_poll.
+// Bulk re-verify from disk (include/vx_hash.h).
+//
+// Pieces up to kChunkBytes: the reader threads pread each slot's pieces
+// straight into that slot's pinned stage (segments back to back,
+// file_store.rs:240-298 byte ranges) and the slot launches while the next free
+// slot is read.  Longer pieces: resumable chunked hashing — round k reads
+// chunk k of every piece of a window into a slot, and the chunk kernel
+// continues each piece's 20-byte SHA-1 state from round k-1, so PCIe moves
+// round k+1 while the GPU compresses round k and no launch waits on a whole
+// multi-MiB chain.  Completions are consumed here; they never reach vx_poll.
+namespace {
+constexpr uint64_t kChunkBytes = 256 * 1024;
+
+struct FileVerify {
+    vx_ctx* c;
+    const uint8_t* expected;
+    uint8_t* matched_out;
+    std::vector<uint8_t>& bad;
+    uint64_t done = 0;
+
+    void consume() {
+        while (!c->done.empty()) {
+            const vx_completion& r = c->done.front();
+            matched_out[r.tag] = (r.matched && !bad[r.tag]) ? 1 : 0;
+            c->done.pop_front();
+            ++done;
+        }
+    }
+    int free_slot() {
+        for (;;) {
+            for (int k = 0; k < (int)c->slots.size(); ++k)
+                if (c->slots[k].state == Slot::FREE) return k;
+            int rc = reap(c, true);
+            consume();
+            if (rc) return rc;
+        }
+    }
+};
+
+int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl, uint64_t total) {
+    vx_ctx* c = fv.c;
+    const uint64_t stride = align_up(pl, kAlign);
+    const uint64_t last_len = total - (n - 1) * (uint64_t)pl;
+    std::vector<vx_files::ReadItem> items;
+    uint64_t next = 0;
+    int rc = 0;
+    while (next < n && !rc) {
+        const int si = fv.free_slot();
+        if (si < 0) return si;
+        Slot& s = c->slots[si];
+        reset_fill(s);
+        const uint64_t cap = std::min<uint64_t>(s.cap, std::max<uint64_t>(1, s.arena_cap / stride));
+        const uint64_t lo = next, hi = std::min<uint64_t>(n, next + cap);
+        items.clear();
+        for (uint64_t i = lo; i < hi; ++i) {
+            const uint32_t len = (uint32_t)(i == n - 1 ? last_len : pl);
+            const uint32_t k = (uint32_t)(i - lo);
+            items.push_back(vx_files::ReadItem{s.h_stage + k * stride, i, 0, len});
+            s.h_offsets[k] = k * stride;
+            s.h_lens[k] = len;
+            if (len != s.h_lens[0]) s.uniform = false;
+            std::memcpy(s.h_expected + (size_t)k * 20, fv.expected + 20 * i, 20);
+            s.tags.push_back(i);
+        }
+        rd.run(items);
+        s.n = (uint32_t)(hi - lo);
+        s.has_expected = true;
+        s.bytes = (hi - lo - 1) * stride + s.h_lens[s.n - 1];
+        s.runs.push_back(Run{0, s.bytes});
+        s.state = Slot::FILLING;
+        rc = launch_slot(c, si);
+        next = hi;
+        if (!rc) rc = reap(c, false);
+        fv.consume();
+    }
+    return rc;
+}
+
+int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl, uint64_t total) {
+    vx_ctx* c = fv.c;
+    const uint64_t C = kChunkBytes;
+    const uint64_t last_len = total - (n - 1) * (uint64_t)pl;
+    // device-side per-piece state, expected table, outputs (indexed by piece)
+    uint32_t* d_states = nullptr;
+    uint8_t *d_exp = nullptr, *d_dig = nullptr, *d_match = nullptr;
+    hipEvent_t prev_kernel = nullptr, ev = nullptr;
+    int rc = 0;
+    auto cleanup = [&]() {
+        for (auto& s : c->slots)
+            if (s.stream) (void)hipStreamSynchronize(s.stream);
+        if (d_states) (void)hipFree(d_states);
+        if (d_exp) (void)hipFree(d_exp);
+        if (d_dig) (void)hipFree(d_dig);
+        if (d_match) (void)hipFree(d_match);
+        if (ev) (void)hipEventDestroy(ev);
+        if (prev_kernel) (void)hipEventDestroy(prev_kernel);
+    };
+    if (hipMalloc(&d_states, n * 20) != hipSuccess || hipMalloc(&d_exp, n * 20) != hipSuccess ||
+        hipMalloc(&d_dig, n * 20) != hipSuccess || hipMalloc(&d_match, n) != hipSuccess) {
+        cleanup();
+        return fail(VX_ENOMEM, "vx_verify_files: device allocation failed");
+    }
+    if (hipMemcpy(d_exp, fv.expected, n * 20, hipMemcpyHostToDevice) != hipSuccess ||
+        hipEventCreateWithFlags(&prev_kernel, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+        cleanup();
+        return fail(VX_EDEVICE, "vx_verify_files: setup failed");
+    }
+    bool have_prev = false;
+    std::vector<vx_files::ReadItem> items;
+    // windows of W pieces; each window runs its rounds in order
+    const Slot& s0 = c->slots[0];
+    const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>(s0.cap, s0.arena_cap / C));
+    for (uint64_t w0 = 0; w0 < n && !rc; w0 += W) {
+        const uint64_t w1 = std::min<uint64_t>(n, w0 + W);
+        const uint64_t rounds = (pl + C - 1) / C;
+        for (uint64_t k = 0; k < rounds && !rc; ++k) {
+            const int si = fv.free_slot();
+            if (si < 0) {
+                rc = si;
+                break;
+            }
+            Slot& s = c->slots[si];
+            reset_fill(s);
+            items.clear();
+            uint32_t m = 0;
+            for (uint64_t i = w0; i < w1; ++i) {
+                const uint64_t len_i = i == n - 1 ? last_len : pl;
+                const uint64_t a = k * C;
+                if (a >= len_i && !(a == 0 && len_i == 0)) continue;  // piece already finished
+                const uint64_t clen = std::min<uint64_t>(C, len_i - a);
+                items.push_back(vx_files::ReadItem{s.h_stage + (uint64_t)m * C, i, a, clen});
+                s.h_offsets[m] = (uint64_t)m * C;
+                s.h_lens[m] = (uint32_t)clen;
+                s.h_pidx[m] = (uint32_t)i;
+                s.h_poff[m] = a;
+                s.h_tlen[m] = len_i;
+                ++m;
+            }
+            if (m == 0) continue;
+            rd.run(items);
+            s.n = m;
+            s.bytes = (uint64_t)(m - 1) * C + s.h_lens[m - 1];
+            s.runs.push_back(Run{0, s.bytes});
+            // H2D in launch order (copy chain), then the chunk kernel after the
+            // previous round's kernel (state dependency), then a done event.
+            hipStream_t st = s.stream;
+            if (c->last_launched >= 0 && c->last_launched != si)
+                rc = hipStreamWaitEvent(st, c->slots[c->last_launched].copied, 0) == hipSuccess ? 0 : VX_EDEVICE;
+            if (!rc && (hipMemcpyAsync(s.d_arena, s.h_stage, s.bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
+                        hipMemcpyAsync(s.d_offsets, s.h_offsets, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+                        hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)m * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+                        hipMemcpyAsync(s.d_pidx, s.h_pidx, (size_t)m * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+                        hipMemcpyAsync(s.d_poff, s.h_poff, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+                        hipMemcpyAsync(s.d_tlen, s.h_tlen, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+                        hipEventRecord(s.copied, st) != hipSuccess))
+                rc = fail(VX_EDEVICE, "vx_verify_files: chunk H2D failed");
+            c->last_launched = si;
+            if (!rc && k > 0 && have_prev && hipStreamWaitEvent(st, prev_kernel, 0) != hipSuccess)
+                rc = fail(VX_EDEVICE, "vx_verify_files: stream wait failed");
+            if (!rc) {
+                hipError_t e = vx::launch_chunk(s.d_arena, s.d_offsets, s.d_lens, m, s.d_pidx, s.d_poff, s.d_tlen,
+                                                d_states, d_dig, d_exp, d_match, st);
+                if (e != hipSuccess) rc = hip_fail(e, "chunk kernel launch");
+            }
+            if (!rc && (hipEventRecord(prev_kernel, st) != hipSuccess || hipEventRecord(s.done, st) != hipSuccess))
+                rc = fail(VX_EDEVICE, "vx_verify_files: event record failed");
+            have_prev = true;
+            s.state = Slot::INFLIGHT;
+            s.seq = c->seq++;
+            s.n = 0;  // nothing to harvest: outputs live in d_match / d_dig
+            if (!rc) rc = reap(c, false);
+        }
+        have_prev = false;  // windows are independent
+    }
+    if (!rc) {
+        for (auto& s : c->slots)
+            if (s.state == Slot::INFLIGHT && hipEventSynchronize(s.done) != hipSuccess) rc = VX_EDEVICE;
+        if (rc) (void)fail(rc, "vx_verify_files: chunk batch failed on device");
+    }
+    if (!rc && hipMemcpy(fv.matched_out, d_match, n, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = fail(VX_EDEVICE, "vx_verify_files: verdict D2H failed");
+    if (!rc)
+        for (uint64_t i = 0; i < n; ++i)
+            if (fv.bad[i]) fv.matched_out[i] = 0;
+    for (auto& s : c->slots)
+        if (s.state == Slot::INFLIGHT) {
+            (void)hipEventSynchronize(s.done);
+            reset_fill(s);
+            s.state = Slot::FREE;
+        }
+    fv.done = n;
+    cleanup();
+    return rc;
+}
+}  // namespace
+
 int64_t vx_verify_files(vx_ctx* c, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
                         uint32_t piece_length, const uint8_t* expected, size_t n_pieces, uint8_t* matched_out,
                         uint32_t io_threads) {
@@ -602,12 +800,14 @@ int64_t vx_verify_files(vx_ctx* c, const char* const* paths, const uint64_t* fil
         return fail(VX_EINVAL, "vx_verify_files: bad argument");
     if (c->sticky) return c->sticky;
     if (c->pending || c->filling >= 0) return fail(VX_EBUSY, "vx_verify_files: async pieces pending");
-    if (piece_length > c->cfg.max_piece_len) return fail(VX_ERANGE, "vx_verify_files: piece_length > max_piece_len");
     uint64_t total = 0;
     for (size_t f = 0; f < nfiles; ++f) total += file_lengths[f];
     if (n_pieces != (total + piece_length - 1) / piece_length)
         return fail(VX_EINVAL, "vx_verify_files: n_pieces does not match the files' total length");
     if (n_pieces == 0) return 0;
+    const bool chunked = piece_length > kChunkBytes;
+    if (chunked ? c->slots[0].arena_cap < kChunkBytes : piece_length > c->cfg.max_piece_len)
+        return fail(VX_ERANGE, "vx_verify_files: pieces do not fit the context's slots");
     int rc = set_device(c);
     if (rc) return rc;
 
@@ -618,54 +818,19 @@ int64_t vx_verify_files(vx_ctx* c, const char* const* paths, const uint64_t* fil
                                     : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<uint8_t> bad(n_pieces, 0);
     std::memset(matched_out, 0, n_pieces);
-    const uint64_t stride = align_up(piece_length, kAlign);
-    uint64_t next = 0, done = 0;
     {
-        vx_files::Readers rd(nthreads, fs, fds, piece_length, n_pieces, total);
-        auto consume = [&]() {
-            while (!c->done.empty()) {
-                const vx_completion& r = c->done.front();
-                matched_out[r.tag] = (r.matched && !bad[r.tag]) ? 1 : 0;
-                c->done.pop_front();
-                ++done;
-            }
-        };
-        while (done < n_pieces && !rc) {
-            int si = -1;
-            if (next < n_pieces)
-                for (int k = 0; k < (int)c->slots.size(); ++k)
-                    if (c->slots[k].state == Slot::FREE) {
-                        si = k;
-                        break;
-                    }
-            if (si < 0) {  // nothing to read into: wait for the oldest batch
+        vx_files::Readers rd(nthreads, fs, fds, piece_length, bad.data());
+        FileVerify fv{c, expected, matched_out, bad};
+        rc = chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total)
+                     : verify_whole(fv, rd, n_pieces, piece_length, total);
+        if (!rc && !chunked) {
+            while (fv.done < n_pieces && !rc) {
                 rc = reap(c, true);
-                consume();
-                continue;
+                fv.consume();
+                bool any = false;
+                for (auto& s : c->slots) any |= s.state == Slot::INFLIGHT;
+                if (!any && fv.done < n_pieces && !rc) rc = fail(VX_EDEVICE, "vx_verify_files: lost completions");
             }
-            Slot& s = c->slots[si];
-            reset_fill(s);
-            const uint64_t cap = std::min<uint64_t>(s.cap, std::max<uint64_t>(1, s.arena_cap / stride));
-            const uint64_t lo = next, hi = std::min<uint64_t>(n_pieces, next + cap);
-            rd.start(lo, hi, s.h_stage, stride, bad.data());
-            rd.wait();
-            for (uint64_t i = lo; i < hi; ++i) {
-                const uint32_t k = (uint32_t)(i - lo);
-                s.h_offsets[k] = k * stride;
-                s.h_lens[k] = rd.piece_len(i);
-                if (s.h_lens[k] != s.h_lens[0]) s.uniform = false;
-                std::memcpy(s.h_expected + (size_t)k * 20, expected + 20 * i, 20);
-                s.tags.push_back(i);
-            }
-            s.n = (uint32_t)(hi - lo);
-            s.has_expected = true;
-            s.bytes = (hi - lo - 1) * stride + s.h_lens[s.n - 1];
-            s.runs.push_back(Run{0, s.bytes});
-            s.state = Slot::FILLING;
-            rc = launch_slot(c, si);
-            next = hi;
-            if (!rc) rc = reap(c, false);
-            consume();
         }
         if (rc) {
             for (auto& s : c->slots)

@@ -85,13 +85,40 @@ inline bool read_full(int fd, uint8_t* dst, int64_t off, int64_t len) {
     return true;
 }
 
-// A fixed pool of reader threads; fill(lo, hi) preads pieces [lo, hi).
+// One read job: bytes [start, start+len) of piece `piece` (a sub-range of
+// the piece's concatenated segments) into dst.
+struct ReadItem {
+    uint8_t* dst;
+    uint64_t piece;
+    uint64_t start;
+    uint64_t len;
+};
+
+// Bytes [start, start+len) of a piece, mapped onto its file segments.
+inline bool read_range(const std::vector<FileSpan>& fs, const std::vector<int>& fds, uint32_t piece_length,
+                       const ReadItem& it, std::vector<Seg>& segs) {
+    segments(fs, (int64_t)it.piece, piece_length, segs);
+    int64_t pos = 0, at = 0;
+    const int64_t a = (int64_t)it.start, b = (int64_t)(it.start + it.len);
+    for (const Seg& s : segs) {
+        const int64_t lo = std::max<int64_t>(a, pos), hi = std::min<int64_t>(b, pos + s.len);
+        if (lo < hi) {
+            if (!read_full(fds[s.file], it.dst + at, s.off + (lo - pos), hi - lo)) return false;
+            at += hi - lo;
+        }
+        pos += s.len;
+    }
+    return at == (int64_t)it.len;  // short: the files end before the piece does
+}
+
+// A fixed pool of reader threads; run(items) preads every item, marking
+// bad[piece] = 1 on any I/O error or short read, and returns when all are done.
 class Readers {
   public:
     Readers(int n, const std::vector<FileSpan>& fs, const std::vector<int>& fds, uint32_t piece_length,
-            uint64_t n_pieces, uint64_t total_len)
-        : fs_(fs), fds_(fds), pl_(piece_length), np_(n_pieces), total_(total_len) {
-        for (int t = 0; t < n; ++t) th_.emplace_back([this] { run(); });
+            uint8_t* bad)
+        : fs_(fs), fds_(fds), pl_(piece_length), bad_(bad) {
+        for (int t = 0; t < n; ++t) th_.emplace_back([this] { loop(); });
     }
     ~Readers() {
         {
@@ -101,59 +128,38 @@ class Readers {
         cv_.notify_all();
         for (auto& t : th_) t.join();
     }
-    void start(uint64_t lo, uint64_t hi, uint8_t* buf, uint64_t stride, uint8_t* bad) {
-        std::lock_guard<std::mutex> g(mu_);
-        lo_ = lo;
-        hi_ = hi;
-        buf_ = buf;
-        stride_ = stride;
-        bad_ = bad;
-        next_.store(lo);
-        left_ = hi - lo;
-        ++gen_;
+    void run(const std::vector<ReadItem>& items) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            items_ = &items;
+            next_.store(0);
+            left_ = items.size();
+            ++gen_;
+        }
         cv_.notify_all();
-    }
-    void wait() {
         std::unique_lock<std::mutex> g(mu_);
         done_cv_.wait(g, [&] { return left_ == 0; });
     }
-    uint32_t piece_len(uint64_t i) const {
-        const uint64_t last = total_ % pl_ ? total_ % pl_ : pl_;
-        return i == np_ - 1 ? (uint32_t)last : pl_;
-    }
 
   private:
-    void run() {
+    void loop() {
         std::vector<Seg> segs;
         uint64_t seen = 0;
         for (;;) {
-            uint64_t lo, hi, stride;
-            uint8_t *buf, *bad;
+            const std::vector<ReadItem>* items;
             {
                 std::unique_lock<std::mutex> g(mu_);
                 cv_.wait(g, [&] { return stop_ || gen_ != seen; });
                 if (stop_) return;
                 seen = gen_;
-                lo = lo_;
-                hi = hi_;
-                buf = buf_;
-                stride = stride_;
-                bad = bad_;
+                items = items_;
             }
             uint64_t mine = 0;
             for (;;) {
-                const uint64_t i = next_.fetch_add(1);
-                if (i >= hi) break;
-                segments(fs_, (int64_t)i, pl_, segs);
-                uint8_t* dst = buf + (i - lo) * stride;
-                bool ok = true;
-                int64_t at = 0;
-                for (const Seg& s : segs) {
-                    ok = ok && read_full(fds_[s.file], dst + at, s.off, s.len);
-                    at += s.len;
-                }
-                ok = ok && at == (int64_t)piece_len(i);
-                bad[i] = ok ? 0 : 1;
+                const uint64_t k = next_.fetch_add(1);
+                if (k >= items->size()) break;
+                const ReadItem& it = (*items)[k];
+                if (!read_range(fs_, fds_, pl_, it, segs)) bad_[it.piece] = 1;
                 ++mine;
             }
             std::lock_guard<std::mutex> g(mu_);
@@ -165,13 +171,13 @@ class Readers {
     const std::vector<FileSpan>& fs_;
     const std::vector<int>& fds_;
     const uint32_t pl_;
-    const uint64_t np_, total_;
+    uint8_t* bad_;
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
     bool stop_ = false;
-    uint64_t gen_ = 0, lo_ = 0, hi_ = 0, stride_ = 0, left_ = 0;
-    uint8_t *buf_ = nullptr, *bad_ = nullptr;
+    uint64_t gen_ = 0, left_ = 0;
+    const std::vector<ReadItem>* items_ = nullptr;
     std::atomic<uint64_t> next_{0};
 };
 

@@ -36,6 +36,14 @@ hipError_t launch_ragged_split(const uint8_t* base, const uint64_t* offsets, con
                                const uint32_t* order, uint32_t n, uint8_t* digests, const uint8_t* expected,
                                uint8_t* matched, hipStream_t stream, const uint32_t* exp_index = nullptr);
 
+// Resumable chunk kernel: lane j hashes bytes
+// [poffs[j], poffs[j]+lens[j]) of piece pids[j] (total tlens[j]) from/to
+// states[pid*5..]; the chunk that ends a piece emits digests/matched row pid
+// (expected row pid).  Non-final chunk lengths must be multiples of 64.
+hipError_t launch_chunk(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens, uint32_t n,
+                        const uint32_t* pids, const uint64_t* poffs, const uint64_t* tlens, uint32_t* states,
+                        uint8_t* digests, const uint8_t* expected, uint8_t* matched, hipStream_t stream);
+
 hipError_t launch_synth_fill(uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint64_t first,
                              uint64_t seed, uint32_t corrupt_every, hipStream_t stream);
 
