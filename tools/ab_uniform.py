@@ -35,7 +35,7 @@ def main():
     for v in variants:
         d, _ = vdev.sha1_uniform(data, n, plen, stride=stride, variant=v)
         torch.cuda.synchronize()
-        if v >= 6:  # diagnostic variants compute different digests on purpose
+        if v == 6:  # diagnostic variant computes different digests on purpose
             continue
         if ref is None:
             ref = d.clone()

@@ -858,7 +858,8 @@ int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t
     if ((reinterpret_cast<uintptr_t>(d_base) & 15) || (stride & 15))
         return fail(VX_EINVAL, "vx_sha1_device_uniform: base and stride must be 16-byte aligned");
     if (n > 1 && stride < len) return fail(VX_EINVAL, "vx_sha1_device_uniform: stride < len");
-    if (variant < 0 || variant > 2) return fail(VX_EINVAL, "vx_sha1_device_uniform: unknown variant");
+    if (variant < 0 || variant > 2)
+        return fail(VX_EINVAL, "vx_sha1_device_uniform: unknown variant");
     hipError_t e = vx::launch_uniform(static_cast<const uint8_t*>(d_base), stride, len, n,
                                       static_cast<uint8_t*>(d_digests), static_cast<const uint8_t*>(d_expected),
                                       static_cast<uint8_t*>(d_matched), static_cast<hipStream_t>(stream), variant);

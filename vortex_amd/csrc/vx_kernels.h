@@ -7,7 +7,8 @@
 namespace vx {
 
 constexpr int kBlock = 256;  // 4 waves = one wave per SIMD of a CU
-constexpr int kRing = 3;     // 128-byte groups in the per-lane register ring
+constexpr int kRing = 3;      // 128-byte groups in the ragged lane kernel's register ring
+constexpr int kLaneRing = 4;  // ... and in the uniform lane kernel's (fenced, exact vmcnt)
 constexpr int kPairBlock = 128;  // split kernel: consumer wave + producer wave
 
 // Uniform-batch kernel variants (vx_tuning.h): 0 = default (best measured),
