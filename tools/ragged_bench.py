@@ -36,6 +36,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--variants", default="1,2")
     a = ap.parse_args()
     import torch
 
@@ -65,9 +66,11 @@ def main():
         d_len = torch.from_numpy(lens).to(dev)
         order = vdev.length_order(lens).to(dev)
         ref = None
-        times = {1: [], 2: []}
+        variants = [int(v) for v in a.variants.split(",")]
+        names = {1: "lane", 2: "split", 11: "split_opaque"}
+        times = {v: [] for v in variants}
         for r in range(a.rounds + 1):
-            for v in (1, 2):
+            for v in variants:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 dig, _ = vdev.sha1_ragged(data, d_off, d_len, order=order, variant=v)
@@ -79,9 +82,9 @@ def main():
                 if r:
                     times[v].append(e0.elapsed_time(e1))
         res = {}
-        for v in (1, 2):
+        for v in variants:
             med = statistics.median(times[v])
-            res["lane" if v == 1 else "split"] = {"median_ms": round(med, 3),
+            res[names.get(v, str(v))] = {"median_ms": round(med, 3),
                                                   "GiBps": round(total / (med * 1e-3) / (1 << 30), 1)}
         out[name] = {"pieces": int(len(lens)), "bytes": int(total), "results": res}
         del data, d_off, d_len, ref
