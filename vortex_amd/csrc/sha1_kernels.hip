@@ -139,6 +139,15 @@ __device__ __forceinline__ void emit(const State& s, uint32_t idx, uint8_t* __re
     }
 }
 
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t u = __shfl_xor(v, o, 64);
+        v = u < v ? u : v;
+    }
+    return v;
+}
+
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -458,36 +467,85 @@ __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
     const uint32_t rem = len & 63u;
     const uint32_t nb = final_chunk ? nfull + (rem <= 55 ? 1u : 2u) : nfull;
     const uint32_t nb_wave = __builtin_amdgcn_readfirstlane(wave_max(nb));
+    // Phase 1 [0, b1): every lane of the wave has a full data block, so the
+    // producer streams a fenced block ring with no per-lane branch and the
+    // consumer commits unconditionally.  Phase 2 [b1, nb_wave): per-lane
+    // data / padding / idle (a few blocks when the wave's lengths differ).
+    constexpr int R = kBlockRing;
+    const uint32_t nfull_min = __builtin_amdgcn_readfirstlane(wave_min(nfull));
+    const uint32_t b1 = nfull_min / R * R;
 
     if (wave == 1) {
         // ---------------- producer ----------------
-        constexpr int R = kBlockRing;
         const uint4* src = nfull ? reinterpret_cast<const uint4*>(p) : g_zero_line;
         const uint32_t last = nfull ? nfull - 1 : 0;
         const uint8_t* q = p + (size_t)nfull * 64;
-        uint4 ring[R][4];
         uint32_t w[16];
+        if (b1) {
+            uint4 ring[R][4];
 #pragma unroll
-        for (int r = 0; r < R - 1; ++r) {
-            const uint32_t bl = (uint32_t)r < last ? (uint32_t)r : last;
-            load_block(ring[r], src + (size_t)bl * 4);
-        }
-        for (uint32_t b0 = 0; b0 < nb_wave; b0 += R) {
+            for (int r = 0; r < R - 1; ++r) {
+                __builtin_amdgcn_sched_barrier(0);
+                load_block(ring[r], src + (size_t)r * 4);
+            }
+            for (uint32_t b0 = 0; b0 < b1; b0 += R) {
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const uint32_t b = b0 + r;
-                const uint32_t bl_raw = b + R - 1;
-                const uint32_t bl = bl_raw < last ? bl_raw : last;
-                load_block(ring[(r + R - 1) % R], src + (size_t)bl * 4);
-                if (b < nb_wave) {
-                    if (b < nfull) {
-                        le_words(w, ring[r][0], ring[r][1], ring[r][2], ring[r][3]);
-                    } else {
-                        // padding blocks (final chunks; other lanes are idle here)
-                        pad_words(w, q, rem, tlen, b - nfull);
-                    }
-                    expand_store(w, lds.w[b & 1], lane);
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t bl_raw = b0 + r + R - 1;
+                    const uint32_t bl = bl_raw < last ? bl_raw : last;
+                    __builtin_amdgcn_sched_barrier(0);
+                    load_block(ring[(r + R - 1) % R], src + (size_t)bl * 4);
+                    __builtin_amdgcn_sched_barrier(0);
+                    le_words(w, ring[r][0], ring[r][1], ring[r][2], ring[r][3]);
+                    expand_store(w, lds.w[(b0 + r) & 1], lane);
                     __syncthreads();
+                }
+            }
+        }
+        if (b1 < nb_wave) {
+            // Phase 2: same fenced ring (clamped to each lane's last data
+            // block), then a per-lane select between the data words, the
+            // padding words (built once, before the loop: no byte loads in
+            // the loop) and zeros for lanes already past their piece.
+            uint32_t padw[16];
+            tail_words(padw, q, rem);
+            const uint32_t bits_hi = (uint32_t)((tlen * 8u) >> 32);
+            const uint32_t bits_lo = (uint32_t)(tlen * 8u);
+            if (rem <= 55) {
+                padw[14] = bits_hi;
+                padw[15] = bits_lo;
+            }
+            uint4 ring[R][4];
+#pragma unroll
+            for (int r = 0; r < R - 1; ++r) {
+                const uint32_t bl_raw = b1 + r;
+                const uint32_t bl = bl_raw < last ? bl_raw : last;
+                __builtin_amdgcn_sched_barrier(0);
+                load_block(ring[r], src + (size_t)bl * 4);
+            }
+            for (uint32_t b0 = b1; b0 < nb_wave; b0 += R) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const uint32_t b = b0 + r;
+                    const uint32_t bl_raw = b + R - 1;
+                    const uint32_t bl = bl_raw < last ? bl_raw : last;
+                    __builtin_amdgcn_sched_barrier(0);
+                    load_block(ring[(r + R - 1) % R], src + (size_t)bl * 4);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (b < nb_wave) {  // wave-uniform
+                        le_words(w, ring[r][0], ring[r][1], ring[r][2], ring[r][3]);
+                        const bool is_pad0 = b == nfull;
+                        const bool is_pad1 = b == nfull + 1;
+#pragma unroll
+                        for (int k = 0; k < 16; ++k) {
+                            uint32_t v = b < nfull ? w[k] : 0u;
+                            v = is_pad0 ? padw[k] : v;
+                            if (k >= 14) v = (is_pad1 && rem > 55) ? (k == 14 ? bits_hi : bits_lo) : v;
+                            w[k] = v;
+                        }
+                        expand_store(w, lds.w[b & 1], lane);
+                        __syncthreads();
+                    }
                 }
             }
         }
@@ -500,7 +558,11 @@ __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
             s = State{st[0], st[1], st[2], st[3], st[4]};
         }
         __syncthreads();
-        for (uint32_t b = 0; b < nb_wave; ++b) {
+        for (uint32_t b = 0; b < b1; ++b) {
+            rounds_lds(s, lds.w[b & 1], lane);
+            __syncthreads();
+        }
+        for (uint32_t b = b1; b < nb_wave; ++b) {
             State t = s;
             rounds_lds(t, lds.w[b & 1], lane);
             if (b < nb) s = t;
