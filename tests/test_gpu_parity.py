@@ -458,3 +458,47 @@ def test_verify_files_chunked(built, gpu, tmp_path, pl, slot_mib, batch):
     want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
     assert got == want
     assert not all(got) and any(got)
+
+
+def test_api_misuse_and_lifecycle(built, gpu):
+    """Errors are codes, never aborts: busy-state checks, bad rows, and
+    destroy with work in flight (drains like the reference's scope join)."""
+    import ctypes
+    import mmap
+
+    from vortex_amd import _lib
+    from vortex_amd._lib import VX_EBUSY, VX_EINVAL, VxError
+    from vortex_amd.hash_pool import HashPool
+
+    pl = 65536
+    pool = HashPool(pl, slots=2, batch_pieces=4)
+    buf = mmap.mmap(-1, pl * 8)
+    pool.register_buffer(buf)
+    body = oracle.gen_piece(1, 0, pl)
+    buf[:pl] = body
+    pool.spawn(0, 1, memoryview(buf)[:pl], pl, hashlib.sha1(body).digest())
+    with pytest.raises(VxError) as e:
+        pool.unregister_buffer(buf)  # piece in flight
+    assert e.value.code == VX_EBUSY
+    with pytest.raises(VxError) as e:
+        pool.verify_batch([body], [bytes(20)])  # sync batch while async pending
+    assert e.value.code == VX_EBUSY
+    with pytest.raises(VxError) as e:
+        pool.set_piece_table(bytes(40))  # table swap while pending
+    assert e.value.code == VX_EBUSY
+    pool.drain()
+    r = pool.try_recv()
+    assert r.hash_matched and r.index == 0
+    pool.set_piece_table(bytes(40))
+    with pytest.raises(VxError) as e:
+        pool.spawn(5, 1, bytearray(10), 10)  # row 5 outside a 2-row table
+    assert e.value.code == VX_EINVAL
+    L = _lib.lib()
+    assert L.vx_register_host_buffer(pool._h, ctypes.c_void_p(ctypes.addressof(
+        ctypes.c_char.from_buffer(buf)) + 100), 10) == VX_EINVAL  # overlaps the registration
+    pool.unregister_buffer(buf)
+    # destroy with pieces still queued and in flight: no crash, drains first
+    for i in range(6):
+        pool.spawn(i, 2, bytearray(body), pl, hashlib.sha1(body).digest())
+    pool.close()
+    assert L.vx_poll(None, None, 0) == VX_EINVAL

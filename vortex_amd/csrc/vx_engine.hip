@@ -204,7 +204,17 @@ void reset_fill(Slot& s) {
     s.use_table = false;
 }
 
+int launch_slot_impl(vx_ctx* c, int si);
+
+// A failed launch leaves a slot half-enqueued: the context turns sticky and
+// every later call reports the error (vx_destroy still cleans up).
 int launch_slot(vx_ctx* c, int si) {
+    const int rc = launch_slot_impl(c, si);
+    if (rc) c->sticky = rc;
+    return rc;
+}
+
+int launch_slot_impl(vx_ctx* c, int si) {
     Slot& s = c->slots[si];
     if (c->filling == si) c->filling = -1;
     if (s.n == 0) {
