@@ -158,6 +158,14 @@ int vx_verify_batch(vx_ctx* ctx, const uint8_t* const* ptrs, const uint32_t* len
 int64_t vx_verify_files(vx_ctx* ctx, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
                         uint32_t piece_length, const uint8_t* expected, size_t n_pieces, uint8_t* matched_out,
                         uint32_t io_threads);
+/* Pieces [first, first+count) of the same torrent only: one rank's shard of a
+ * multi-GPU re-verify (python: vortex_amd.shard.verify_files_sharded).
+ * expected is still the whole n_pieces*20 table; matched_out has count
+ * bytes, matched_out[k] for piece first+k.  Only that range's bytes are read.
+ * vx_verify_files(...) is vx_verify_files_range(..., 0, n_pieces, ...). */
+int64_t vx_verify_files_range(vx_ctx* ctx, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
+                              uint32_t piece_length, const uint8_t* expected, size_t n_pieces, size_t first,
+                              size_t count, uint8_t* matched_out, uint32_t io_threads);
 
 /* ---- device-resident batches (the hot path; no context needed) -------- */
 /* Pieces i in [0,n) at d_base + i*stride, each len bytes.  Writes

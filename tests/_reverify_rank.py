@@ -1,0 +1,36 @@
+"""One rank of the multi-GPU re-verify test (tests/test_gpu_reverify_shard.py).
+
+Launched by torch.distributed.run; every rank opens a HashPool on its GPU
+(LOCAL_RANK modulo the visible devices, so two ranks share cuda:0 on a
+one-GPU box), verifies its shard with vx_verify_files_range and gathers the
+verdicts (shard.verify_files_sharded).  Rank 0 writes the result as JSON.
+"""
+import json
+import os
+import sys
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vortex_amd import shard  # noqa: E402
+from vortex_amd.hash_pool import HashPool  # noqa: E402
+
+
+def main():
+    spec = json.load(open(sys.argv[1]))
+    backend = sys.argv[3] if len(sys.argv) > 3 else "gloo"
+    dev = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
+    torch.cuda.set_device(dev)
+    dist.init_process_group(backend)
+    with HashPool(spec["piece_length"], device=dev, slots=3, batch_pieces=8, slot_bytes=4 << 20) as pool:
+        got, bad = shard.verify_files_sharded(pool, spec["paths"], spec["sizes"], spec["piece_length"],
+                                              bytes.fromhex(spec["expected"]), io_threads=3)
+    if dist.get_rank() == 0:
+        with open(sys.argv[2], "w") as f:
+            json.dump({"matched": got, "bad": bad, "world": dist.get_world_size()}, f)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

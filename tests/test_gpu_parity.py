@@ -301,6 +301,34 @@ def test_config5_linux_mint_geometry(built, gpu, golden):
     assert int(matched2.sum()) == n
 
 
+def test_pieces_over_512MiB(built, gpu):
+    """Maximum sizes: a piece of 512 MiB + 77 B has a bit length above 2^32,
+    so the 64-bit length field's high word is nonzero (FIPS 180-4 5.1.1).
+    Uniform path (2 pieces) and ragged path (with a short and an empty piece)."""
+    import torch
+
+    from vortex_amd import device as vdev
+
+    dev = torch.device("cuda:0")
+    seed, L = 0x5EED0B16, (512 << 20) + 77
+    stride = (L + 255) // 256 * 256
+    data = torch.empty(2 * stride, dtype=torch.uint8, device=dev)
+    vdev.synth_fill(data, 2, L, stride=stride, seed=seed)
+    dig, _ = vdev.sha1_uniform(data, 2, L, stride=stride)
+    torch.cuda.synchronize()
+    want = oracle.pool_digest_synth(seed, 0, 2, L, threads=2)
+    assert bytes(dig.cpu().numpy().tobytes()) == want
+    # ragged: piece 1's first 100 bytes are synthetic piece (seed, 1, 100)
+    offs = torch.tensor([0, stride, stride], dtype=torch.int64, device=dev)
+    lens = torch.tensor([L, 100, 0], dtype=torch.int32, device=dev)
+    dig2, _ = vdev.sha1_ragged(data, offs, lens, order=vdev.length_order([L, 100, 0]).to(dev))
+    torch.cuda.synchronize()
+    got = dig2.cpu().numpy().tobytes()
+    assert got[:20] == want[:20]
+    assert got[20:40] == oracle.sha1(oracle.gen_piece(seed, 1, 100))
+    assert got[40:] == hashlib.sha1(b"").digest()
+
+
 def test_idempotent_and_stream_ordering(built, gpu):
     """Same batch hashed twice on a side stream gives identical digests."""
     import torch

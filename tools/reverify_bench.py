@@ -10,6 +10,11 @@ geometry of cli/linux-mint.torrent (2,907,832,320 B, 2 MiB pieces, last
 synthetic data (and every piece must match).
 
 usage: python tools/reverify_bench.py [--dir /tmp] [--scale 1.0] [--reps 3]
+
+Under torch.distributed.run (WORLD_SIZE > 1) every rank verifies its shard of
+the pieces on its own GPU (shard.verify_files_sharded): the
+time is the max over ranks, bracketed by barriers, and the CPU leg is skipped.
+Rank 0 writes the file; ranks on one host read the same page cache.
 """
 import argparse
 import json
@@ -33,7 +38,11 @@ def main():
     a = ap.parse_args()
     import ctypes
 
-    import torch  # noqa: F401  (single HIP runtime)
+    import torch  # (single HIP runtime)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        return dist_main(a, world)
 
     import oracle
     from vortex_amd.hash_pool import HashPool
@@ -75,6 +84,56 @@ def main():
     if not a.keep:
         os.unlink(path)
     print(json.dumps(res))
+
+
+def dist_main(a, world):
+    import ctypes
+
+    import torch
+    import torch.distributed as dist
+
+    import oracle
+    from vortex_amd import shard
+    from vortex_amd.hash_pool import HashPool
+
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dev = local % torch.cuda.device_count()
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo")  # verdict gather of a few KiB; the payload never crosses ranks
+    rank = dist.get_rank()
+    pl = 2097152
+    total = 2907832320 if a.scale >= 1.0 else int(2907832320 * a.scale) // pl * pl + 1179648
+    n = (total + pl - 1) // pl
+    last = total - (n - 1) * pl
+    threads = a.threads or max(1, min(16, len(os.sched_getaffinity(0))) // world)
+    path = os.path.join(a.dir, "vx_linuxmint_synth.iso")
+    if rank == 0:
+        buf = ctypes.create_string_buffer(pl)
+        with open(path, "wb") as f:
+            for i in range(n):
+                L = last if i == n - 1 else pl
+                oracle.lib().vxo_gen_piece(0x5EED0005, i, L, 0, buf)
+                f.write(buf.raw[:L])
+    exp = oracle.pool_digest_synth(0x5EED0005, 0, n, pl, last_index=n - 1, last_len=last, threads=threads)
+    dist.barrier()
+    runs = []
+    with HashPool(pl, device=dev, slots=a.slots, slot_bytes=a.slot_mib << 20, batch_pieces=4096) as pool:
+        for rep in range(a.reps):
+            dist.barrier()
+            t0 = time.perf_counter()
+            got, bad = shard.verify_files_sharded(pool, [path], [total], pl, exp, io_threads=threads)
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            assert all(got) and bad == 0
+            runs.append({"gpu_e2e_GiBps": round(total / t.item() / float(1 << 30), 2), "s": round(t.item(), 3)})
+    dist.barrier()
+    if rank == 0:
+        print(json.dumps({"workload": f"sharded re-verify {n} x 2 MiB pieces ({total} B) over {world} ranks",
+                          "ranks": world, "gpus": torch.cuda.device_count(), "threads_per_rank": threads,
+                          "runs": runs, "best_GiBps": max(r["gpu_e2e_GiBps"] for r in runs)}))
+        if not a.keep:
+            os.unlink(path)
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

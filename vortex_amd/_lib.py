@@ -31,7 +31,7 @@ EXPORTS = (
     "vx_abi_version", "vx_last_error", "vx_strerror", "vx_device_count", "vx_config_default",
     "vx_create", "vx_destroy", "vx_register_host_buffer", "vx_unregister_host_buffer",
     "vx_submit", "vx_flush", "vx_poll", "vx_drain", "vx_pending", "vx_set_piece_table", "vx_submit_piece",
-    "vx_sha1_batch", "vx_verify_batch", "vx_verify_files",
+    "vx_sha1_batch", "vx_verify_batch", "vx_verify_files", "vx_verify_files_range",
     "vx_sha1_device_uniform", "vx_sha1_device_ragged", "vx_sort_order",
     "vx_synth_fill", "vx_sha1_device_uniform_variant", "vx_sha1_device_ragged_variant",
 )
@@ -80,6 +80,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "vx_sha1_batch": ([vp, vp, vp, c.c_size_t, vp], c.c_int),
         "vx_verify_batch": ([vp, vp, vp, vp, c.c_size_t, vp, vp], c.c_int),
         "vx_verify_files": ([vp, vp, vp, c.c_size_t, c.c_uint32, vp, c.c_size_t, vp, c.c_uint32], c.c_int64),
+        "vx_verify_files_range": ([vp, vp, vp, c.c_size_t, c.c_uint32, vp, c.c_size_t, c.c_size_t, c.c_size_t, vp,
+                                   c.c_uint32], c.c_int64),
         "vx_sha1_device_uniform": ([vp, c.c_uint64, c.c_uint32, c.c_uint32, vp, vp, vp, vp], c.c_int),
         "vx_sha1_device_ragged": ([vp, vp, vp, vp, c.c_uint32, vp, vp, vp, vp], c.c_int),
         "vx_sort_order": ([vp, c.c_uint32, vp], c.c_int),

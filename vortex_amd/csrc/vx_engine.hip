@@ -645,20 +645,23 @@ struct FileVerify {
     }
 };
 
-int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl, uint64_t total) {
+// Both verify pieces [first, end) of an n-piece torrent; tags, bad[] and
+// matched_out are indexed from `first`.
+int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl, uint64_t total, uint64_t first,
+                 uint64_t end) {
     vx_ctx* c = fv.c;
     const uint64_t stride = align_up(pl, kAlign);
     const uint64_t last_len = total - (n - 1) * (uint64_t)pl;
     std::vector<vx_files::ReadItem> items;
-    uint64_t next = 0;
+    uint64_t next = first;
     int rc = 0;
-    while (next < n && !rc) {
+    while (next < end && !rc) {
         const int si = fv.free_slot();
         if (si < 0) return si;
         Slot& s = c->slots[si];
         reset_fill(s);
         const uint64_t cap = std::min<uint64_t>(s.cap, std::max<uint64_t>(1, s.arena_cap / stride));
-        const uint64_t lo = next, hi = std::min<uint64_t>(n, next + cap);
+        const uint64_t lo = next, hi = std::min<uint64_t>(end, next + cap);
         items.clear();
         for (uint64_t i = lo; i < hi; ++i) {
             const uint32_t len = (uint32_t)(i == n - 1 ? last_len : pl);
@@ -668,7 +671,7 @@ int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl,
             s.h_lens[k] = len;
             if (len != s.h_lens[0]) s.uniform = false;
             std::memcpy(s.h_expected + (size_t)k * 20, fv.expected + 20 * i, 20);
-            s.tags.push_back(i);
+            s.tags.push_back(i - first);
         }
         rd.run(items);
         s.n = (uint32_t)(hi - lo);
@@ -684,11 +687,13 @@ int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl,
     return rc;
 }
 
-int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl, uint64_t total) {
+int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl, uint64_t total, uint64_t first,
+                   uint64_t end) {
     vx_ctx* c = fv.c;
     const uint64_t C = kChunkBytes;
     const uint64_t last_len = total - (n - 1) * (uint64_t)pl;
-    // device-side per-piece state, expected table, outputs (indexed by piece)
+    const uint64_t cnt = end - first;
+    // device-side per-piece state, expected table, outputs (indexed by piece - first)
     uint32_t* d_states = nullptr;
     uint8_t *d_exp = nullptr, *d_dig = nullptr, *d_match = nullptr;
     hipEvent_t prev_kernel = nullptr, ev = nullptr;
@@ -703,12 +708,12 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
         if (ev) (void)hipEventDestroy(ev);
         if (prev_kernel) (void)hipEventDestroy(prev_kernel);
     };
-    if (hipMalloc(&d_states, n * 20) != hipSuccess || hipMalloc(&d_exp, n * 20) != hipSuccess ||
-        hipMalloc(&d_dig, n * 20) != hipSuccess || hipMalloc(&d_match, n) != hipSuccess) {
+    if (hipMalloc(&d_states, cnt * 20) != hipSuccess || hipMalloc(&d_exp, cnt * 20) != hipSuccess ||
+        hipMalloc(&d_dig, cnt * 20) != hipSuccess || hipMalloc(&d_match, cnt) != hipSuccess) {
         cleanup();
         return fail(VX_ENOMEM, "vx_verify_files: device allocation failed");
     }
-    if (hipMemcpy(d_exp, fv.expected, n * 20, hipMemcpyHostToDevice) != hipSuccess ||
+    if (hipMemcpy(d_exp, fv.expected + 20 * first, cnt * 20, hipMemcpyHostToDevice) != hipSuccess ||
         hipEventCreateWithFlags(&prev_kernel, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
         cleanup();
@@ -719,8 +724,8 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     // windows of W pieces; each window runs its rounds in order
     const Slot& s0 = c->slots[0];
     const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>(s0.cap, s0.arena_cap / C));
-    for (uint64_t w0 = 0; w0 < n && !rc; w0 += W) {
-        const uint64_t w1 = std::min<uint64_t>(n, w0 + W);
+    for (uint64_t w0 = first; w0 < end && !rc; w0 += W) {
+        const uint64_t w1 = std::min<uint64_t>(end, w0 + W);
         const uint64_t rounds = (pl + C - 1) / C;
         for (uint64_t k = 0; k < rounds && !rc; ++k) {
             const int si = fv.free_slot();
@@ -740,7 +745,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
                 items.push_back(vx_files::ReadItem{s.h_stage + (uint64_t)m * C, i, a, clen});
                 s.h_offsets[m] = (uint64_t)m * C;
                 s.h_lens[m] = (uint32_t)clen;
-                s.h_pidx[m] = (uint32_t)i;
+                s.h_pidx[m] = (uint32_t)(i - first);
                 s.h_poff[m] = a;
                 s.h_tlen[m] = len_i;
                 ++m;
@@ -786,10 +791,10 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
             if (s.state == Slot::INFLIGHT && hipEventSynchronize(s.done) != hipSuccess) rc = VX_EDEVICE;
         if (rc) (void)fail(rc, "vx_verify_files: chunk batch failed on device");
     }
-    if (!rc && hipMemcpy(fv.matched_out, d_match, n, hipMemcpyDeviceToHost) != hipSuccess)
+    if (!rc && hipMemcpy(fv.matched_out, d_match, cnt, hipMemcpyDeviceToHost) != hipSuccess)
         rc = fail(VX_EDEVICE, "vx_verify_files: verdict D2H failed");
     if (!rc)
-        for (uint64_t i = 0; i < n; ++i)
+        for (uint64_t i = 0; i < cnt; ++i)
             if (fv.bad[i]) fv.matched_out[i] = 0;
     for (auto& s : c->slots)
         if (s.state == Slot::INFLIGHT) {
@@ -797,49 +802,53 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
             reset_fill(s);
             s.state = Slot::FREE;
         }
-    fv.done = n;
+    fv.done = cnt;
     cleanup();
     return rc;
 }
 }  // namespace
 
-int64_t vx_verify_files(vx_ctx* c, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
-                        uint32_t piece_length, const uint8_t* expected, size_t n_pieces, uint8_t* matched_out,
-                        uint32_t io_threads) {
-    if (!c || (nfiles && (!paths || !file_lengths)) || piece_length == 0 || (n_pieces && (!expected || !matched_out)))
+int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
+                              uint32_t piece_length, const uint8_t* expected, size_t n_pieces, size_t first,
+                              size_t count, uint8_t* matched_out, uint32_t io_threads) {
+    if (!c || (nfiles && (!paths || !file_lengths)) || piece_length == 0 || (n_pieces && !expected) ||
+        (count && !matched_out))
         return fail(VX_EINVAL, "vx_verify_files: bad argument");
+    if (first > n_pieces || count > n_pieces - first)
+        return fail(VX_EINVAL, "vx_verify_files: piece range outside the torrent");
     if (c->sticky) return c->sticky;
     if (c->pending || c->filling >= 0) return fail(VX_EBUSY, "vx_verify_files: async pieces pending");
     uint64_t total = 0;
     for (size_t f = 0; f < nfiles; ++f) total += file_lengths[f];
     if (n_pieces != (total + piece_length - 1) / piece_length)
         return fail(VX_EINVAL, "vx_verify_files: n_pieces does not match the files' total length");
-    if (n_pieces == 0) return 0;
+    if (count == 0) return 0;
     const bool chunked = piece_length > kChunkBytes;
     if (chunked ? c->slots[0].arena_cap < kChunkBytes : piece_length > c->cfg.max_piece_len)
         return fail(VX_ERANGE, "vx_verify_files: pieces do not fit the context's slots");
     int rc = set_device(c);
     if (rc) return rc;
 
+    const uint64_t end = first + count;
     const std::vector<vx_files::FileSpan> fs = vx_files::layout(file_lengths, nfiles, piece_length);
     std::vector<int> fds(nfiles, -1);
     for (size_t f = 0; f < nfiles; ++f) fds[f] = open(paths[f], O_RDONLY | O_CLOEXEC);
     const int nthreads = io_threads ? (int)io_threads
                                     : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-    std::vector<uint8_t> bad(n_pieces, 0);
-    std::memset(matched_out, 0, n_pieces);
+    std::vector<uint8_t> bad(count, 0);
+    std::memset(matched_out, 0, count);
     {
-        vx_files::Readers rd(nthreads, fs, fds, piece_length, bad.data());
+        vx_files::Readers rd(nthreads, fs, fds, piece_length, bad.data(), first);
         FileVerify fv{c, expected, matched_out, bad};
-        rc = chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total)
-                     : verify_whole(fv, rd, n_pieces, piece_length, total);
+        rc = chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total, first, end)
+                     : verify_whole(fv, rd, n_pieces, piece_length, total, first, end);
         if (!rc && !chunked) {
-            while (fv.done < n_pieces && !rc) {
+            while (fv.done < count && !rc) {
                 rc = reap(c, true);
                 fv.consume();
                 bool any = false;
                 for (auto& s : c->slots) any |= s.state == Slot::INFLIGHT;
-                if (!any && fv.done < n_pieces && !rc) rc = fail(VX_EDEVICE, "vx_verify_files: lost completions");
+                if (!any && fv.done < count && !rc) rc = fail(VX_EDEVICE, "vx_verify_files: lost completions");
             }
         }
         if (rc) {
@@ -856,6 +865,13 @@ int64_t vx_verify_files(vx_ctx* c, const char* const* paths, const uint64_t* fil
     int64_t nbad = 0;
     for (uint8_t x : bad) nbad += x;
     return nbad;
+}
+
+int64_t vx_verify_files(vx_ctx* c, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
+                        uint32_t piece_length, const uint8_t* expected, size_t n_pieces, uint8_t* matched_out,
+                        uint32_t io_threads) {
+    return vx_verify_files_range(c, paths, file_lengths, nfiles, piece_length, expected, n_pieces, 0, n_pieces,
+                                 matched_out, io_threads);
 }
 
 int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,

@@ -112,12 +112,13 @@ inline bool read_range(const std::vector<FileSpan>& fs, const std::vector<int>& 
 }
 
 // A fixed pool of reader threads; run(items) preads every item, marking
-// bad[piece] = 1 on any I/O error or short read, and returns when all are done.
+// bad[piece - first] = 1 on any I/O error or short read, and returns when all
+// are done.  `first` is the first piece of the verified range.
 class Readers {
   public:
     Readers(int n, const std::vector<FileSpan>& fs, const std::vector<int>& fds, uint32_t piece_length,
-            uint8_t* bad)
-        : fs_(fs), fds_(fds), pl_(piece_length), bad_(bad) {
+            uint8_t* bad, uint64_t first = 0)
+        : fs_(fs), fds_(fds), pl_(piece_length), bad_(bad), first_(first) {
         for (int t = 0; t < n; ++t) th_.emplace_back([this] { loop(); });
     }
     ~Readers() {
@@ -159,7 +160,7 @@ class Readers {
                 const uint64_t k = next_.fetch_add(1);
                 if (k >= items->size()) break;
                 const ReadItem& it = (*items)[k];
-                if (!read_range(fs_, fds_, pl_, it, segs)) bad_[it.piece] = 1;
+                if (!read_range(fs_, fds_, pl_, it, segs)) bad_[it.piece - first_] = 1;
                 ++mine;
             }
             std::lock_guard<std::mutex> g(mu_);
@@ -172,6 +173,7 @@ class Readers {
     const std::vector<int>& fds_;
     const uint32_t pl_;
     uint8_t* bad_;
+    const uint64_t first_;
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;

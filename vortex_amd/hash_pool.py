@@ -198,12 +198,15 @@ class HashPool:
         return [raw[20 * i: 20 * i + 20] for i in range(n)]
 
     def verify_files(self, paths: Sequence[str], file_lengths: Sequence[int], piece_length: int,
-                     expected: bytes, io_threads: int = 0) -> tuple[list[bool], int]:
+                     expected: bytes, io_threads: int = 0, first: int = 0,
+                     count: int | None = None) -> tuple[list[bool], int]:
         """State::from_metadata_and_root's bulk re-verify (torrent.rs:716-761):
         pieces read from the torrent's files (file_store.rs:228-303 byte
         ranges) and verified on the GPU.  Returns (verdicts, pieces with I/O
-        errors).  `expected` is the torrent's `pieces` string (n*20 bytes)."""
-        return _verify_files(self, paths, file_lengths, piece_length, expected, io_threads)
+        errors).  `expected` is the torrent's `pieces` string (n*20 bytes).
+        first/count restrict it to pieces [first, first+count) (one rank's
+        shard, vx_verify_files_range); the verdicts then cover that range."""
+        return _verify_files(self, paths, file_lengths, piece_length, expected, io_threads, first, count)
 
     def verify_batch(self, pieces: Sequence, expected: Sequence[bytes]) -> tuple[list[bool], list[bytes]]:
         n = len(pieces)
@@ -219,15 +222,22 @@ class HashPool:
 
 
 def _verify_files(pool: "HashPool", paths: Sequence[str], file_lengths: Sequence[int], piece_length: int,
-                  expected: bytes, io_threads: int = 0) -> tuple[list[bool], int]:
+                  expected: bytes, io_threads: int = 0, first: int = 0,
+                  count: int | None = None) -> tuple[list[bool], int]:
     n = len(expected) // 20
+    if count is None:
+        count = n - first
     arr = (ctypes.c_char_p * max(1, len(paths)))(*[os.fsencode(p) for p in paths])
     lens = (ctypes.c_uint64 * max(1, len(file_lengths)))(*file_lengths)
     exp = ctypes.create_string_buffer(bytes(expected), max(1, len(expected)))
-    out = ctypes.create_string_buffer(max(1, n))
-    bad = check(lib().vx_verify_files(pool._h, arr, lens, len(paths), piece_length, exp, n, out, io_threads),
-                "vx_verify_files")
-    return [bool(b) for b in out.raw[:n]], int(bad)
+    out = ctypes.create_string_buffer(max(1, count))
+    if first == 0 and count == n:
+        rc = lib().vx_verify_files(pool._h, arr, lens, len(paths), piece_length, exp, n, out, io_threads)
+    else:
+        rc = lib().vx_verify_files_range(pool._h, arr, lens, len(paths), piece_length, exp, n, first, count, out,
+                                         io_threads)
+    bad = check(rc, "vx_verify_files")
+    return [bool(b) for b in out.raw[:count]], int(bad)
 
 
 def _ptr_arrays(pieces: Sequence):
