@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -116,13 +117,15 @@ struct Slot {
 struct vx_ctx {
     vx_config cfg{};
     std::vector<Slot> slots;
-    // H2D copies are serialised across slots in launch order: each slot's
-    // stream first waits for the previous slot's copies (event), so PCIe
-    // moves one batch at a time at full rate and batch k's kernel starts as
-    // soon as its own bytes are in, while batch k+1 copies.  (Copies racing
-    // on all slot streams share PCIe and delay every kernel; one shared copy
-    // stream would head-of-line block behind kernels on the 4 HW queues.)
-    int last_launched = -1;
+    // H2D copies are serialised across slots in launch order, so PCIe moves
+    // one batch at a time at full rate and batch k's kernel starts as soon as
+    // its own bytes are in, while batch k+1 copies.  (Copies racing on all
+    // slot streams share PCIe and delay every kernel.)  How the order is
+    // enforced is h2d_mode (VX_H2D_MODE, read at vx_create; see chain_h2d).
+    int last_launched = -1;  // slot whose H2D was enqueued last
+    int prev_launched = -1;  // the one before it
+    int h2d_mode = 2;
+    hipStream_t copy_stream = nullptr;  // mode 3 only
     // Device-resident `pieces` table (vx_set_piece_table).
     uint8_t* d_table = nullptr;
     uint32_t n_table = 0;
@@ -206,6 +209,76 @@ void reset_fill(Slot& s) {
 
 int launch_slot_impl(vx_ctx* c, int si);
 
+// Order slot si's H2D after the previously launched slot's (one PCIe stream
+// of copies across all slots).  Modes:
+//   0  the slot stream waits on the previous slot's `copied` event;
+//   1  as 0, and the host first waits for the copy two launches back;
+//   2  the host waits for the previous slot's copy, no cross-stream wait
+//      (default);
+//   3  every H2D on one dedicated copy stream.
+// With 0 and 1, hipMemcpyAsync enqueued behind a cross-stream wait blocked
+// the host for ~8-9 ms at a time early in a run and left PCIe idle
+// (profiles/r01/e2e_first_use/).  A/B on one MI355X, 8192 x 256 KiB through
+// vx_verify_batch: 34-46 / 38-40 / 48.5-48.7 / 45 GiB/s for modes 0-3
+// (profiles/r01/h2d_modes/).  Mode 2 keeps copies back to back with a gap of
+// one host wake-up, and blocks the host for at most one batch's copy.
+int chain_h2d(vx_ctx* c, int si) {
+    const int last = c->last_launched, prev = c->prev_launched;
+    const int mode = c->h2d_mode;
+    if (mode == 3) return 0;
+    if (mode == 1 && prev >= 0 && prev != si && prev != last) VX_HIP(hipEventSynchronize(c->slots[prev].copied));
+    if (mode == 2) {
+        if (last >= 0 && last != si) VX_HIP(hipEventSynchronize(c->slots[last].copied));
+        return 0;
+    }
+    if (last >= 0 && last != si) VX_HIP(hipStreamWaitEvent(c->slots[si].stream, c->slots[last].copied, 0));
+    return 0;
+}
+
+void mark_launched(vx_ctx* c, int si) {
+    if (c->last_launched != si) c->prev_launched = c->last_launched;
+    c->last_launched = si;
+}
+
+// Run every command type a batch uses once on every slot stream, in the
+// launch pattern of launch_slot_impl (cross-slot copy chain, large and small
+// H2D, both default kernels, D2H).  The HIP runtime sets up the hardware
+// queues and copy paths behind a stream on first use, and that blocked the
+// host for ~8 ms inside hipMemcpyAsync on the first two slots of the first
+// batches (profiles/r01/e2e_first_use/); paying it here keeps it off the
+// batch path.
+int warm_slots(vx_ctx* c) {
+    int prev = -1;
+    for (int si = 0; si < (int)c->slots.size(); ++si) {
+        Slot& s = c->slots[si];
+        hipStream_t st = s.stream;
+        if (prev >= 0) VX_HIP(hipStreamWaitEvent(st, c->slots[prev].copied, 0));
+        VX_HIP(hipMemcpyAsync(s.d_arena, s.h_stage, std::min<uint64_t>(s.arena_cap, 8ull << 20),
+                              hipMemcpyHostToDevice, st));
+        VX_HIP(hipMemcpyAsync(s.d_expected, s.h_expected, 20, hipMemcpyHostToDevice, st));
+        VX_HIP(hipEventRecord(s.copied, st));
+        hipError_t e = vx::launch_uniform(s.d_arena, kAlign, 64, 1, s.d_digests, s.d_expected, s.d_matched, st,
+                                          vx::kUniformDefault, nullptr);
+        if (e == hipSuccess) {
+            s.h_offsets[0] = 0;
+            s.h_lens[0] = 64;
+            VX_HIP(hipMemcpyAsync(s.d_offsets, s.h_offsets, 8, hipMemcpyHostToDevice, st));
+            VX_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, 4, hipMemcpyHostToDevice, st));
+            e = vx::launch_ragged(s.d_arena, s.d_offsets, s.d_lens, nullptr, 1, s.d_digests, s.d_expected,
+                                  s.d_matched, st, vx::kUniformDefault, nullptr);
+        }
+        if (e != hipSuccess) return hip_fail(e, "vx_create: warm-up launch");
+        VX_HIP(hipMemcpyAsync(s.h_digests, s.d_digests, 20, hipMemcpyDeviceToHost, st));
+        VX_HIP(hipMemcpyAsync(s.h_matched, s.d_matched, 1, hipMemcpyDeviceToHost, st));
+        VX_HIP(hipEventRecord(s.done, st));
+        prev = si;
+    }
+    for (auto& s : c->slots) VX_HIP(hipStreamSynchronize(s.stream));
+    c->last_launched = prev;
+    c->prev_launched = -1;
+    return 0;
+}
+
 // A failed launch leaves a slot half-enqueued: the context turns sticky and
 // every later call reports the error (vx_destroy still cleans up).
 int launch_slot(vx_ctx* c, int si) {
@@ -221,9 +294,8 @@ int launch_slot_impl(vx_ctx* c, int si) {
         s.state = Slot::FREE;
         return 0;
     }
-    hipStream_t cs = s.stream;
-    if (c->last_launched >= 0 && c->last_launched != si)
-        VX_HIP(hipStreamWaitEvent(cs, c->slots[c->last_launched].copied, 0));
+    hipStream_t cs = c->h2d_mode == 3 ? c->copy_stream : s.stream;
+    if (int rc = chain_h2d(c, si)) return rc;
     for (const DirectRun& r : s.druns)
         VX_HIP(hipMemcpyAsync(s.d_arena + r.lo, r.host, r.hi - r.lo, hipMemcpyHostToDevice, cs));
     for (const Run& r : s.runs)
@@ -240,7 +312,8 @@ int launch_slot_impl(vx_ctx* c, int si) {
         VX_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)n * 4, hipMemcpyHostToDevice, cs));
     }
     VX_HIP(hipEventRecord(s.copied, cs));
-    c->last_launched = si;
+    if (cs != s.stream) VX_HIP(hipStreamWaitEvent(s.stream, s.copied, 0));
+    mark_launched(c, si);
     hipError_t e;
     if (s.uniform) {
         const uint32_t len = s.h_lens[0];
@@ -426,7 +499,10 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     vx_ctx* c = new (std::nothrow) vx_ctx();
     if (!c) return fail(VX_ENOMEM, "vx_create: out of host memory");
     c->cfg = *cfg;
+    if (const char* m = std::getenv("VX_H2D_MODE")) c->h2d_mode = std::atoi(m) & 3;
     int rc = set_device(c);
+    if (!rc && c->h2d_mode == 3 && hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess)
+        rc = fail(VX_EDEVICE, "vx_create: copy stream");
     if (!rc) {
         c->slots.resize(cfg->slots);
         for (auto& s : c->slots) {
@@ -434,8 +510,10 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
             if (rc) break;
         }
     }
+    if (!rc) rc = warm_slots(c);
     if (rc) {
         for (auto& s : c->slots) free_slot_mem(s);
+        if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
         delete c;
         return rc;
     }
@@ -449,6 +527,7 @@ int vx_destroy(vx_ctx* c) {
     set_device(c);
     for (auto& r : c->registered) (void)hipHostUnregister(reinterpret_cast<void*>(r.first));
     for (auto& s : c->slots) free_slot_mem(s);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->d_table) (void)hipFree(c->d_table);
     delete c;
     return rc;
@@ -583,10 +662,13 @@ static int batch_impl(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* len
             if ((size_t)k < buf.size()) return 0;
         }
     };
+    // Completions are harvested by acquire_filling when it runs out of slots;
+    // polling here between submits would only add event queries to the
+    // launch path, so the queue is drained only when it grows large.
     for (size_t i = 0; i < n; ++i) {
         rc = submit_impl(c, i, ptrs[i], lens[i], expected ? expected + i * 20 : nullptr);
         if (rc) return rc;
-        if ((i & 255) == 255 && (rc = collect())) return rc;
+        if (c->done.size() >= 65536 && (rc = collect())) return rc;
     }
     if ((rc = vx_drain(c, 0))) return rc;
     if ((rc = collect())) return rc;
@@ -758,8 +840,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
             // H2D in launch order (copy chain), then the chunk kernel after the
             // previous round's kernel (state dependency), then a done event.
             hipStream_t st = s.stream;
-            if (c->last_launched >= 0 && c->last_launched != si)
-                rc = hipStreamWaitEvent(st, c->slots[c->last_launched].copied, 0) == hipSuccess ? 0 : VX_EDEVICE;
+            rc = chain_h2d(c, si);
             if (!rc && (hipMemcpyAsync(s.d_arena, s.h_stage, s.bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
                         hipMemcpyAsync(s.d_offsets, s.h_offsets, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
                         hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)m * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
@@ -768,7 +849,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
                         hipMemcpyAsync(s.d_tlen, s.h_tlen, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
                         hipEventRecord(s.copied, st) != hipSuccess))
                 rc = fail(VX_EDEVICE, "vx_verify_files: chunk H2D failed");
-            c->last_launched = si;
+            mark_launched(c, si);
             if (!rc && k > 0 && have_prev && hipStreamWaitEvent(st, prev_kernel, 0) != hipSuccess)
                 rc = fail(VX_EDEVICE, "vx_verify_files: stream wait failed");
             if (!rc) {
