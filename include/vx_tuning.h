@@ -16,6 +16,12 @@ extern "C" {
 int vx_sha1_device_ragged_variant(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
                                   const uint32_t* d_order, uint32_t n, void* d_digests, const void* d_expected,
                                   void* d_matched, void* stream, int variant);
+/* Chunk rounds a context has launched on the resumable chunk paths (file
+ * re-verify of pieces > 256 KiB, strided host batches).
+ * Tests use it to tell which path a batch took. */
+struct vx_ctx;
+uint64_t vx_tuning_chunk_rounds(const struct vx_ctx* ctx);
+
 int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
                                    const void* d_expected, void* d_matched, void* stream, int variant);
 

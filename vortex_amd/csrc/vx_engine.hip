@@ -125,6 +125,15 @@ struct vx_ctx {
     int last_launched = -1;  // slot whose H2D was enqueued last
     int prev_launched = -1;  // the one before it
     int h2d_mode = 2;
+    // Chunk bytes for strided host batches of long pieces (§6.4); 0 = off.
+    uint64_t batch_chunk = 64 * 1024;
+    uint64_t chunk_rounds = 0;  // chunk rounds launched (vx_tuning_chunk_rounds)
+    // Per-piece device rows of the chunk paths (state | expected | digest |
+    // verdict), kept across calls and grown on demand: allocating them per
+    // call cost ~1 ms of a 40 ms e2e batch.
+    uint8_t* d_chunk_rows = nullptr;
+    uint64_t chunk_rows_cap = 0;
+    hipEvent_t chunk_prev = nullptr;
     hipStream_t copy_stream = nullptr;  // mode 3 only
     // Device-resident `pieces` table (vx_set_piece_table).
     uint8_t* d_table = nullptr;
@@ -138,6 +147,14 @@ struct vx_ctx {
 };
 
 namespace {
+
+// Pieces (lanes) a slot's metadata holds: the async batch size, or enough
+// chunk lanes to fill the arena with kMinChunk-byte chunks (the chunked paths
+// of §6.3/§6.4 put one chunk per lane), whichever is larger.
+constexpr uint64_t kMinChunk = 64 * 1024;
+uint32_t slot_capacity(const vx_config* cfg) {
+    return (uint32_t)std::min<uint64_t>(1u << 20, std::max<uint64_t>(cfg->batch_pieces, cfg->slot_bytes / kMinChunk));
+}
 
 int set_device(const vx_ctx* c) {
     VX_HIP(hipSetDevice(c->cfg.device));
@@ -500,13 +517,14 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (!c) return fail(VX_ENOMEM, "vx_create: out of host memory");
     c->cfg = *cfg;
     if (const char* m = std::getenv("VX_H2D_MODE")) c->h2d_mode = std::atoi(m) & 3;
+    if (const char* m = std::getenv("VX_BATCH_CHUNK")) c->batch_chunk = align_up(std::strtoull(m, nullptr, 0), kAlign);
     int rc = set_device(c);
     if (!rc && c->h2d_mode == 3 && hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess)
         rc = fail(VX_EDEVICE, "vx_create: copy stream");
     if (!rc) {
         c->slots.resize(cfg->slots);
         for (auto& s : c->slots) {
-            rc = alloc_slot(s, cfg->slot_bytes, cfg->batch_pieces);
+            rc = alloc_slot(s, cfg->slot_bytes, slot_capacity(cfg));
             if (rc) break;
         }
     }
@@ -529,6 +547,8 @@ int vx_destroy(vx_ctx* c) {
     for (auto& s : c->slots) free_slot_mem(s);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->d_table) (void)hipFree(c->d_table);
+    if (c->d_chunk_rows) (void)hipFree(c->d_chunk_rows);
+    if (c->chunk_prev) (void)hipEventDestroy(c->chunk_prev);
     delete c;
     return rc;
 }
@@ -640,54 +660,6 @@ int vx_drain(vx_ctx* c, uint32_t timeout_ms) {
 
 uint64_t vx_pending(const vx_ctx* c) { return c ? c->pending : 0; }
 
-static int batch_impl(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, const uint8_t* expected, size_t n,
-                      uint8_t* matched_out, uint8_t* digests_out) {
-    if (!c) return fail(VX_EINVAL, "batch: NULL context");
-    if (n && (!ptrs || !lens)) return fail(VX_EINVAL, "batch: NULL ptrs/lens");
-    if (c->pending) return fail(VX_EBUSY, "batch: async pieces pending; drain and poll first");
-    int rc = set_device(c);
-    if (rc) return rc;
-    std::vector<vx_completion> buf(1024);
-    size_t got = 0;
-    auto collect = [&]() -> int {
-        for (;;) {
-            int64_t k = vx_poll(c, buf.data(), buf.size());
-            if (k < 0) return (int)k;
-            for (int64_t j = 0; j < k; ++j) {
-                const vx_completion& r = buf[j];
-                if (digests_out) std::memcpy(digests_out + r.tag * 20, r.digest, 20);
-                if (matched_out) matched_out[r.tag] = r.matched;
-            }
-            got += (size_t)k;
-            if ((size_t)k < buf.size()) return 0;
-        }
-    };
-    // Completions are harvested by acquire_filling when it runs out of slots;
-    // polling here between submits would only add event queries to the
-    // launch path, so the queue is drained only when it grows large.
-    for (size_t i = 0; i < n; ++i) {
-        rc = submit_impl(c, i, ptrs[i], lens[i], expected ? expected + i * 20 : nullptr);
-        if (rc) return rc;
-        if (c->done.size() >= 65536 && (rc = collect())) return rc;
-    }
-    if ((rc = vx_drain(c, 0))) return rc;
-    if ((rc = collect())) return rc;
-    if (got != n) return fail(VX_EDEVICE, "batch: lost completions");
-    return 0;
-}
-
-int vx_sha1_batch(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, size_t n, uint8_t* digests_out) {
-    if (!digests_out && n) return fail(VX_EINVAL, "vx_sha1_batch: NULL digests_out");
-    return batch_impl(c, ptrs, lens, nullptr, n, nullptr, digests_out);
-}
-
-int vx_verify_batch(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, const uint8_t* expected, size_t n,
-                    uint8_t* matched_out, uint8_t* digests_out) {
-    if (n && (!expected || !matched_out)) return fail(VX_EINVAL, "vx_verify_batch: NULL expected/matched_out");
-    return batch_impl(c, ptrs, lens, expected, n, matched_out, digests_out);
-}
-
-
 // Bulk re-verify from disk (include/vx_hash.h).
 //
 // Pieces up to kChunkBytes: the reader threads pread each slot's pieces
@@ -698,6 +670,8 @@ int vx_verify_batch(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens,
 // continues each piece's 20-byte SHA-1 state from round k-1, so PCIe moves
 // round k+1 while the GPU compresses round k and no launch waits on a whole
 // multi-MiB chain.  Completions are consumed here; they never reach vx_poll.
+}  // extern "C" (the helpers below are C++ templates)
+
 namespace {
 constexpr uint64_t kChunkBytes = 256 * 1024;
 
@@ -769,48 +743,144 @@ int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl,
     return rc;
 }
 
+// Resumable chunk pipeline, shared by the file
+// re-verify and strided host batches.  The call owns per-piece device rows
+// (chaining state, expected digest, digest, verdict).  Each round is one slot:
+// its H2D joins the copy chain across slots (chain_h2d), and its kernel waits
+// for the previous round of the same window (state dependency) through
+// `prev_kernel`, so PCIe moves round k+1 while the GPU compresses round k.
+struct ChunkPipe {
+    vx_ctx* c;
+    uint64_t cnt = 0;
+    uint32_t* d_states = nullptr;
+    uint8_t *d_exp = nullptr, *d_dig = nullptr, *d_match = nullptr;
+    hipEvent_t prev_kernel = nullptr;
+    bool have_prev = false;
+
+    explicit ChunkPipe(vx_ctx* ctx) : c(ctx) {}
+    ~ChunkPipe() { release(); }
+    ChunkPipe(const ChunkPipe&) = delete;
+    ChunkPipe& operator=(const ChunkPipe&) = delete;
+
+    // expected: count x 20 bytes or NULL (digests only).
+    int open(uint64_t count, const uint8_t* expected, const char* who) {
+        cnt = count;
+        if (c->chunk_rows_cap < count) {
+            if (c->d_chunk_rows) (void)hipFree(c->d_chunk_rows);
+            c->d_chunk_rows = nullptr;
+            c->chunk_rows_cap = 0;
+            const uint64_t cap = std::max<uint64_t>(count, 4096);
+            if (hipMalloc(&c->d_chunk_rows, cap * 61 + 256) != hipSuccess)
+                return fail(VX_ENOMEM, std::string(who) + ": device allocation failed");
+            c->chunk_rows_cap = cap;
+        }
+        const uint64_t cap = c->chunk_rows_cap;
+        d_states = reinterpret_cast<uint32_t*>(c->d_chunk_rows);
+        d_dig = c->d_chunk_rows + cap * 20;
+        d_exp = expected ? c->d_chunk_rows + cap * 40 : nullptr;
+        d_match = expected ? c->d_chunk_rows + cap * 60 : nullptr;
+        if (!c->chunk_prev && hipEventCreateWithFlags(&c->chunk_prev, hipEventDisableTiming) != hipSuccess)
+            return fail(VX_EDEVICE, std::string(who) + ": event creation failed");
+        prev_kernel = c->chunk_prev;
+        if (expected && hipMemcpy(d_exp, expected, cnt * 20, hipMemcpyHostToDevice) != hipSuccess)
+            return fail(VX_EDEVICE, std::string(who) + ": expected-table upload failed");
+        return 0;
+    }
+
+    // A free slot, reaping the oldest round when none is; on_reap runs after
+    // every blocking reap (the file path consumes whole-piece completions).
+    template <class F>
+    int free_slot(F&& on_reap) {
+        for (;;) {
+            for (int k = 0; k < (int)c->slots.size(); ++k)
+                if (c->slots[k].state == Slot::FREE) return k;
+            int rc = reap(c, true);
+            on_reap();
+            if (rc) return rc;
+        }
+    }
+
+    // Slot si's h_offsets/h_lens/h_pidx/h_poff/h_tlen [0, m) describe the
+    // round's lanes; copy_data(slot, stream) enqueues the chunk bytes into
+    // the slot arena.  continues = the round follows one of the same window.
+    template <class F>
+    int round(int si, uint32_t m, bool continues, F&& copy_data) {
+        Slot& s = c->slots[si];
+        hipStream_t st = s.stream;
+        int rc = chain_h2d(c, si);
+        if (!rc) rc = copy_data(s, st);
+        if (!rc && (hipMemcpyAsync(s.d_offsets, s.h_offsets, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+                    hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)m * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+                    hipMemcpyAsync(s.d_pidx, s.h_pidx, (size_t)m * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
+                    hipMemcpyAsync(s.d_poff, s.h_poff, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+                    hipMemcpyAsync(s.d_tlen, s.h_tlen, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+                    hipEventRecord(s.copied, st) != hipSuccess))
+            rc = fail(VX_EDEVICE, "chunk round: H2D failed");
+        mark_launched(c, si);
+        if (!rc && continues && have_prev && hipStreamWaitEvent(st, prev_kernel, 0) != hipSuccess)
+            rc = fail(VX_EDEVICE, "chunk round: stream wait failed");
+        if (!rc) {
+            hipError_t e = vx::launch_chunk(s.d_arena, s.d_offsets, s.d_lens, m, s.d_pidx, s.d_poff, s.d_tlen,
+                                            d_states, d_dig, d_exp, d_match, st);
+            if (e != hipSuccess) rc = hip_fail(e, "chunk kernel launch");
+        }
+        if (!rc && (hipEventRecord(prev_kernel, st) != hipSuccess || hipEventRecord(s.done, st) != hipSuccess))
+            rc = fail(VX_EDEVICE, "chunk round: event record failed");
+        have_prev = true;
+        c->chunk_rounds++;
+        s.state = Slot::INFLIGHT;
+        s.seq = c->seq++;
+        s.n = 0;  // nothing to harvest: outputs live in the call's device rows
+        if (!rc) rc = reap(c, false);
+        return rc;
+    }
+    void end_window() { have_prev = false; }  // windows hold disjoint pieces
+
+    // Wait for every round, then copy verdicts / digests back (either may be NULL).
+    int finish(uint8_t* matched_out, uint8_t* digests_out, int rc) {
+        if (!rc) {
+            for (auto& s : c->slots)
+                if (s.state == Slot::INFLIGHT && hipEventSynchronize(s.done) != hipSuccess) rc = VX_EDEVICE;
+            if (rc) (void)fail(rc, "chunk rounds failed on device");
+        }
+        if (!rc && matched_out && d_match && hipMemcpy(matched_out, d_match, cnt, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = fail(VX_EDEVICE, "verdict D2H failed");
+        if (!rc && digests_out && hipMemcpy(digests_out, d_dig, cnt * 20, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = fail(VX_EDEVICE, "digest D2H failed");
+        for (auto& s : c->slots)
+            if (s.state == Slot::INFLIGHT) {
+                (void)hipEventSynchronize(s.done);
+                reset_fill(s);
+                s.state = Slot::FREE;
+            }
+        return rc;
+    }
+
+    // The rows and the event belong to the context (freed by vx_destroy);
+    // only make sure nothing of this call is still running.
+    void release() {
+        for (auto& s : c->slots)
+            if (s.stream) (void)hipStreamSynchronize(s.stream);
+    }
+};
+
 int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl, uint64_t total, uint64_t first,
                    uint64_t end) {
     vx_ctx* c = fv.c;
     const uint64_t C = kChunkBytes;
     const uint64_t last_len = total - (n - 1) * (uint64_t)pl;
     const uint64_t cnt = end - first;
-    // device-side per-piece state, expected table, outputs (indexed by piece - first)
-    uint32_t* d_states = nullptr;
-    uint8_t *d_exp = nullptr, *d_dig = nullptr, *d_match = nullptr;
-    hipEvent_t prev_kernel = nullptr, ev = nullptr;
-    int rc = 0;
-    auto cleanup = [&]() {
-        for (auto& s : c->slots)
-            if (s.stream) (void)hipStreamSynchronize(s.stream);
-        if (d_states) (void)hipFree(d_states);
-        if (d_exp) (void)hipFree(d_exp);
-        if (d_dig) (void)hipFree(d_dig);
-        if (d_match) (void)hipFree(d_match);
-        if (ev) (void)hipEventDestroy(ev);
-        if (prev_kernel) (void)hipEventDestroy(prev_kernel);
-    };
-    if (hipMalloc(&d_states, cnt * 20) != hipSuccess || hipMalloc(&d_exp, cnt * 20) != hipSuccess ||
-        hipMalloc(&d_dig, cnt * 20) != hipSuccess || hipMalloc(&d_match, cnt) != hipSuccess) {
-        cleanup();
-        return fail(VX_ENOMEM, "vx_verify_files: device allocation failed");
-    }
-    if (hipMemcpy(d_exp, fv.expected + 20 * first, cnt * 20, hipMemcpyHostToDevice) != hipSuccess ||
-        hipEventCreateWithFlags(&prev_kernel, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
-        cleanup();
-        return fail(VX_EDEVICE, "vx_verify_files: setup failed");
-    }
-    bool have_prev = false;
+    ChunkPipe cp(c);
+    int rc = cp.open(cnt, fv.expected + 20 * first, "vx_verify_files");
     std::vector<vx_files::ReadItem> items;
     // windows of W pieces; each window runs its rounds in order
     const Slot& s0 = c->slots[0];
     const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>(s0.cap, s0.arena_cap / C));
+    const uint64_t rounds = (pl + C - 1) / C;
     for (uint64_t w0 = first; w0 < end && !rc; w0 += W) {
         const uint64_t w1 = std::min<uint64_t>(end, w0 + W);
-        const uint64_t rounds = (pl + C - 1) / C;
         for (uint64_t k = 0; k < rounds && !rc; ++k) {
-            const int si = fv.free_slot();
+            const int si = cp.free_slot([&] { fv.consume(); });
             if (si < 0) {
                 rc = si;
                 break;
@@ -834,60 +904,158 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
             }
             if (m == 0) continue;
             rd.run(items);
-            s.n = m;
             s.bytes = (uint64_t)(m - 1) * C + s.h_lens[m - 1];
-            s.runs.push_back(Run{0, s.bytes});
-            // H2D in launch order (copy chain), then the chunk kernel after the
-            // previous round's kernel (state dependency), then a done event.
-            hipStream_t st = s.stream;
-            rc = chain_h2d(c, si);
-            if (!rc && (hipMemcpyAsync(s.d_arena, s.h_stage, s.bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
-                        hipMemcpyAsync(s.d_offsets, s.h_offsets, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
-                        hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)m * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
-                        hipMemcpyAsync(s.d_pidx, s.h_pidx, (size_t)m * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
-                        hipMemcpyAsync(s.d_poff, s.h_poff, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
-                        hipMemcpyAsync(s.d_tlen, s.h_tlen, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
-                        hipEventRecord(s.copied, st) != hipSuccess))
-                rc = fail(VX_EDEVICE, "vx_verify_files: chunk H2D failed");
-            mark_launched(c, si);
-            if (!rc && k > 0 && have_prev && hipStreamWaitEvent(st, prev_kernel, 0) != hipSuccess)
-                rc = fail(VX_EDEVICE, "vx_verify_files: stream wait failed");
-            if (!rc) {
-                hipError_t e = vx::launch_chunk(s.d_arena, s.d_offsets, s.d_lens, m, s.d_pidx, s.d_poff, s.d_tlen,
-                                                d_states, d_dig, d_exp, d_match, st);
-                if (e != hipSuccess) rc = hip_fail(e, "chunk kernel launch");
-            }
-            if (!rc && (hipEventRecord(prev_kernel, st) != hipSuccess || hipEventRecord(s.done, st) != hipSuccess))
-                rc = fail(VX_EDEVICE, "vx_verify_files: event record failed");
-            have_prev = true;
-            s.state = Slot::INFLIGHT;
-            s.seq = c->seq++;
-            s.n = 0;  // nothing to harvest: outputs live in d_match / d_dig
-            if (!rc) rc = reap(c, false);
+            rc = cp.round(si, m, k > 0, [&](Slot& sl, hipStream_t st) {
+                if (hipMemcpyAsync(sl.d_arena, sl.h_stage, sl.bytes, hipMemcpyHostToDevice, st) != hipSuccess)
+                    return fail(VX_EDEVICE, "vx_verify_files: chunk H2D failed");
+                return 0;
+            });
         }
-        have_prev = false;  // windows are independent
+        cp.end_window();
     }
-    if (!rc) {
-        for (auto& s : c->slots)
-            if (s.state == Slot::INFLIGHT && hipEventSynchronize(s.done) != hipSuccess) rc = VX_EDEVICE;
-        if (rc) (void)fail(rc, "vx_verify_files: chunk batch failed on device");
-    }
-    if (!rc && hipMemcpy(fv.matched_out, d_match, cnt, hipMemcpyDeviceToHost) != hipSuccess)
-        rc = fail(VX_EDEVICE, "vx_verify_files: verdict D2H failed");
+    rc = cp.finish(fv.matched_out, nullptr, rc);
     if (!rc)
         for (uint64_t i = 0; i < cnt; ++i)
             if (fv.bad[i]) fv.matched_out[i] = 0;
-    for (auto& s : c->slots)
-        if (s.state == Slot::INFLIGHT) {
-            (void)hipEventSynchronize(s.done);
-            reset_fill(s);
-            s.state = Slot::FREE;
-        }
     fv.done = cnt;
-    cleanup();
     return rc;
 }
+
+// Strided host batches of long pieces: every piece inside
+// one registered range at a constant host stride, all of one length except
+// possibly a shorter last piece — a bulk verify over a contiguous host copy
+// of the torrent (torrent.rs:724-740), or the bench's e2e sample.  Round k of
+// a window moves bytes [k*C, (k+1)*C) of each of its pieces with ONE
+// hipMemcpy2DAsync (source pitch = host stride; 53 GiB/s like a flat copy,
+// profiles/r01/h2d/h2d2d.json), and the chunk kernel continues each piece's
+// state.  So the transfer is back to back and only the last round's short
+// chain trails it, instead of a whole-piece chain per slot.
+bool strided_batch(const vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, size_t n,
+                   uint64_t* host_stride) {
+    const uint64_t C = c->batch_chunk;
+    if (n == 0 || C == 0 || c->slots[0].arena_cap < C) return false;
+    const uint32_t L = lens[0];
+    if (L < 2 * C || L > c->cfg.max_piece_len || lens[n - 1] == 0 || lens[n - 1] > L) return false;
+    const uintptr_t p0 = reinterpret_cast<uintptr_t>(ptrs[0]);
+    const uintptr_t hs = n > 1 ? reinterpret_cast<uintptr_t>(ptrs[1]) - p0 : L;
+    if (hs < L || hs > (1ull << 40)) return false;
+    for (size_t i = 0; i + 1 < n; ++i)
+        if (lens[i] != L || reinterpret_cast<uintptr_t>(ptrs[i]) != p0 + i * hs) return false;
+    if (reinterpret_cast<uintptr_t>(ptrs[n - 1]) != p0 + (n - 1) * hs) return false;
+    if (!is_registered(c, ptrs[0], (n - 1) * hs + lens[n - 1])) return false;
+    *host_stride = hs;
+    return true;
+}
+
+int batch_chunked(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, const uint8_t* expected, size_t n,
+                  uint8_t* matched_out, uint8_t* digests_out, uint64_t hs) {
+    const uint64_t C = c->batch_chunk;
+    const uint64_t L = lens[0], Llast = lens[n - 1];
+    const uint8_t* base = ptrs[0];
+    ChunkPipe cp(c);
+    int rc = cp.open(n, expected, "batch");
+    const Slot& s0 = c->slots[0];
+    const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>(s0.cap, s0.arena_cap / C));
+    const uint64_t rounds = (L + C - 1) / C;
+    for (uint64_t w0 = 0; w0 < n && !rc; w0 += W) {
+        const uint64_t w1 = std::min<uint64_t>(n, w0 + W);
+        const bool short_last = w1 == n && Llast != L;
+        const uint64_t full_rows = (w1 - w0) - (short_last ? 1 : 0);
+        for (uint64_t k = 0; k < rounds && !rc; ++k) {
+            const uint64_t a = k * C;
+            const uint64_t width = std::min<uint64_t>(C, L - a);   // every full-length row
+            const uint64_t dpitch = align_up(width, kAlign);       // <= C
+            const uint64_t last_w = short_last && a < Llast ? std::min<uint64_t>(C, Llast - a) : 0;
+            const uint32_t m = (uint32_t)(full_rows + (last_w ? 1 : 0));
+            if (m == 0) continue;
+            const int si = cp.free_slot([] {});
+            if (si < 0) {
+                rc = si;
+                break;
+            }
+            Slot& s = c->slots[si];
+            reset_fill(s);
+            for (uint32_t r = 0; r < m; ++r) {
+                const bool is_last = r == full_rows;
+                s.h_offsets[r] = (uint64_t)r * dpitch;
+                s.h_lens[r] = (uint32_t)(is_last ? last_w : width);
+                s.h_pidx[r] = (uint32_t)(is_last ? n - 1 : w0 + r);
+                s.h_poff[r] = a;
+                s.h_tlen[r] = is_last ? Llast : L;
+            }
+            rc = cp.round(si, m, k > 0, [&](Slot& sl, hipStream_t st) {
+                if (full_rows && hipMemcpy2DAsync(sl.d_arena, dpitch, base + w0 * hs + a, hs, width, full_rows,
+                                                  hipMemcpyHostToDevice, st) != hipSuccess)
+                    return fail(VX_EDEVICE, "batch: chunk 2D H2D failed");
+                if (last_w && hipMemcpyAsync(sl.d_arena + full_rows * dpitch, ptrs[n - 1] + a, last_w,
+                                             hipMemcpyHostToDevice, st) != hipSuccess)
+                    return fail(VX_EDEVICE, "batch: chunk H2D failed");
+                return 0;
+            });
+        }
+        cp.end_window();
+    }
+    return cp.finish(matched_out, digests_out, rc);
+}
 }  // namespace
+
+extern "C" {
+
+static int batch_impl(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, const uint8_t* expected, size_t n,
+                      uint8_t* matched_out, uint8_t* digests_out) {
+    if (!c) return fail(VX_EINVAL, "batch: NULL context");
+    if (n && (!ptrs || !lens)) return fail(VX_EINVAL, "batch: NULL ptrs/lens");
+    if (c->pending) return fail(VX_EBUSY, "batch: async pieces pending; drain and poll first");
+    if (c->sticky) return c->sticky;
+    if (c->filling >= 0) {  // an empty filling slot (pending == 0): hand it back
+        c->slots[c->filling].state = Slot::FREE;
+        c->filling = -1;
+    }
+    int rc = set_device(c);
+    if (rc) return rc;
+    uint64_t host_stride = 0;
+    if (strided_batch(c, ptrs, lens, n, &host_stride))
+        return batch_chunked(c, ptrs, lens, expected, n, matched_out, digests_out, host_stride);
+    std::vector<vx_completion> buf(1024);
+    size_t got = 0;
+    auto collect = [&]() -> int {
+        for (;;) {
+            int64_t k = vx_poll(c, buf.data(), buf.size());
+            if (k < 0) return (int)k;
+            for (int64_t j = 0; j < k; ++j) {
+                const vx_completion& r = buf[j];
+                if (digests_out) std::memcpy(digests_out + r.tag * 20, r.digest, 20);
+                if (matched_out) matched_out[r.tag] = r.matched;
+            }
+            got += (size_t)k;
+            if ((size_t)k < buf.size()) return 0;
+        }
+    };
+    // Completions are harvested by acquire_filling when it runs out of slots;
+    // polling here between submits would only add event queries to the
+    // launch path, so the queue is drained only when it grows large.
+    for (size_t i = 0; i < n; ++i) {
+        rc = submit_impl(c, i, ptrs[i], lens[i], expected ? expected + i * 20 : nullptr);
+        if (rc) return rc;
+        if (c->done.size() >= 65536 && (rc = collect())) return rc;
+    }
+    if ((rc = vx_drain(c, 0))) return rc;
+    if ((rc = collect())) return rc;
+    if (got != n) return fail(VX_EDEVICE, "batch: lost completions");
+    return 0;
+}
+
+int vx_sha1_batch(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, size_t n, uint8_t* digests_out) {
+    if (!digests_out && n) return fail(VX_EINVAL, "vx_sha1_batch: NULL digests_out");
+    return batch_impl(c, ptrs, lens, nullptr, n, nullptr, digests_out);
+}
+
+int vx_verify_batch(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, const uint8_t* expected, size_t n,
+                    uint8_t* matched_out, uint8_t* digests_out) {
+    if (n && (!expected || !matched_out)) return fail(VX_EINVAL, "vx_verify_batch: NULL expected/matched_out");
+    return batch_impl(c, ptrs, lens, expected, n, matched_out, digests_out);
+}
+
 
 int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
                               uint32_t piece_length, const uint8_t* expected, size_t n_pieces, size_t first,
@@ -1003,6 +1171,8 @@ int vx_sha1_device_ragged(const void* d_base, const uint64_t* d_offsets, const u
     return vx_sha1_device_ragged_variant(d_base, d_offsets, d_lens, d_order, n, d_digests, d_expected, d_matched,
                                          stream, 0);
 }
+
+uint64_t vx_tuning_chunk_rounds(const vx_ctx* c) { return c ? c->chunk_rounds : 0; }
 
 int vx_sort_order(const uint32_t* lens, uint32_t n, uint32_t* order_out) {
     if (n && (!lens || !order_out)) return fail(VX_EINVAL, "vx_sort_order: NULL argument");
