@@ -21,6 +21,9 @@ int vx_sha1_device_ragged_variant(const void* d_base, const uint64_t* d_offsets,
  * Tests use it to tell which path a batch took. */
 struct vx_ctx;
 uint64_t vx_tuning_chunk_rounds(const struct vx_ctx* ctx);
+/* 64 KiB tiles the context's gather kernel has pulled from registered host
+ * buffers (async / batch slots). */
+uint64_t vx_tuning_gather_tiles(const struct vx_ctx* ctx);
 
 int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
                                    const void* d_expected, void* d_matched, void* stream, int variant);

@@ -1,0 +1,61 @@
+// readers_stress.cpp — CPU test of vx_files::Readers (the pread pool behind
+// vx_verify_files): many back-to-back run() generations whose item vector the
+// caller rebuilds (and regrows) between runs, as verify_whole / verify_chunked
+// do.  Every item must land the right file bytes.  Built plain and with
+// -fsanitize=thread by tests/test_native_cpu.py; exit 0 = ok.
+//
+// usage: readers_stress <scratch_file> [generations=3000] [threads=6]
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "vx_files.hpp"
+
+int main(int argc, char** argv) {
+    if (argc < 2) return 2;
+    const int gens = argc > 2 ? std::atoi(argv[2]) : 3000;
+    const int nthreads = argc > 3 ? std::atoi(argv[3]) : 6;
+    const uint32_t pl = 4096;
+    const uint32_t npieces = 512;
+    std::vector<uint8_t> file((size_t)pl * npieces);
+    std::mt19937 rng(1);
+    for (auto& b : file) b = (uint8_t)rng();
+    FILE* f = std::fopen(argv[1], "wb");
+    if (!f || std::fwrite(file.data(), 1, file.size(), f) != file.size()) return 2;
+    std::fclose(f);
+    const uint64_t len = file.size();
+    const std::vector<vx_files::FileSpan> fs = vx_files::layout(&len, 1, pl);
+    std::vector<int> fds{open(argv[1], O_RDONLY)};
+    std::vector<uint8_t> bad(npieces, 0);
+    std::vector<uint8_t> stage((size_t)pl * npieces);
+    int errors = 0;
+    {
+        vx_files::Readers rd(nthreads, fs, fds, pl, bad.data(), 0);
+        std::vector<vx_files::ReadItem> items;
+        for (int g = 0; g < gens; ++g) {
+            items.clear();
+            items.shrink_to_fit();  // force a reallocation on every refill
+            const uint32_t m = 1 + rng() % 64;
+            const uint32_t base = rng() % (npieces - m);
+            for (uint32_t k = 0; k < m; ++k) {
+                const uint32_t p = base + k;
+                const uint32_t a = rng() % 2 ? 0 : 1024;
+                items.push_back(vx_files::ReadItem{stage.data() + (size_t)k * pl, p, a, pl - a});
+            }
+            rd.run(items);
+            for (uint32_t k = 0; k < m; ++k) {
+                const auto& it = items[k];
+                if (std::memcmp(it.dst, file.data() + (size_t)it.piece * pl + it.start, it.len) != 0) ++errors;
+            }
+        }
+    }
+    close(fds[0]);
+    for (uint8_t b : bad) errors += b;
+    std::printf("{\"generations\": %d, \"errors\": %d}\n", gens, errors);
+    return errors == 0 ? 0 : 1;
+}

@@ -586,3 +586,84 @@ def test_strided_batch_chunked(built, gpu, monkeypatch, L, hs_extra, n, last_len
         assert _lib.lib().vx_tuning_chunk_rounds(pool._h) == 0
         pool.unregister_buffer(buf)
     assert matched0 == matched and dig0 == want
+
+
+@pytest.mark.parametrize("gather", ["1", "0"])
+def test_scattered_registered_pieces(built, gpu, monkeypatch, gather):
+    """Pieces scattered over a registered pool (buf_pool.rs buffers in no
+    particular order) are pulled by the gather kernel on the
+    async path and on non-strided host batches; unaligned registered pieces
+    fall back to per-piece DMA and unregistered ones to the pinned stage, all
+    in the same batches.  Digests bit-exact vs hashlib/the oracle with the
+    gather kernel on and off (VX_GATHER)."""
+    import mmap
+
+    from vortex_amd import _lib
+    from vortex_amd.hash_pool import HashPool
+
+    monkeypatch.setenv("VX_GATHER", gather)
+    rng = random.Random(5)
+    lens = [0, 1, 15, 16, 17, 63, 64, 65, 4095, 65535, 65536, 65537, 131072 + 48, 200000, (1 << 20) + 3, 300]
+    lens = lens * 6
+    rng.shuffle(lens)
+    slot = 1 << 21  # pool buffer size
+    buf = mmap.mmap(-1, slot * (len(lens) + 8))
+    np.frombuffer(buf, dtype=np.uint8)[:] = np.random.default_rng(9).integers(0, 256, len(buf), dtype=np.uint8)
+    slots = list(range(len(lens) + 8))
+    rng.shuffle(slots)
+    mv = memoryview(buf)
+    pieces = []
+    for k, L in enumerate(lens):
+        start = slots[k] * slot + (0 if k % 7 else 5)  # every 7th piece unaligned -> per-piece DMA
+        pieces.append(mv[start:start + L])
+    extra = [bytearray(oracle.gen_piece(5, k, L)) for k, L in enumerate([70000, 16, 0, 65536])]  # unregistered
+    allp = pieces + extra
+    want = [hashlib.sha1(p).digest() for p in allp]
+    assert want[3] == oracle.sha1(bytes(allp[3]))
+    with HashPool(1 << 21, slots=3, batch_pieces=24, slot_bytes=8 << 20) as pool:
+        pool.register_buffer(buf)
+        t0 = _lib.lib().vx_tuning_gather_tiles(pool._h)
+        for i, p in enumerate(allp):
+            pool.spawn(i, 3, p, len(p), want[i] if i % 9 else bytes(20))
+            if i % 10 == 9:
+                pool.flush()
+        pool.drain()
+        got = {r.index: (r.hash_matched, r.digest) for r in pool.try_iter()}
+        dig = pool.sha1_batch(allp)  # not strided: slot path
+        tiles = _lib.lib().vx_tuning_gather_tiles(pool._h) - t0
+        pool.unregister_buffer(buf)
+    assert len(got) == len(allp)
+    for i in range(len(allp)):
+        assert got[i][1] == want[i], i
+        assert got[i][0] == (i % 9 != 0), i
+    assert dig == want
+    expect_tiles = 2 * sum((L + 65535) // 65536 for k, L in enumerate(lens) if k % 7 and L)
+    assert tiles == (expect_tiles if gather == "1" else 0)
+
+
+def test_lazy_flush_launches_from_poll(built, gpu):
+    """vx_flush leaves the filling slot open when launching it would leave no
+    slot free; polling alone must then launch it once a batch
+    completes, and every piece must come back (no vx_drain)."""
+    import time
+
+    from vortex_amd.hash_pool import HashPool
+
+    pl = 1 << 20
+    pieces = [bytes(oracle.gen_piece(77, i, pl)) for i in range(12)]
+    want = {i: hashlib.sha1(p).digest() for i, p in enumerate(pieces)}
+    got = {}
+    with HashPool(pl, slots=2, batch_pieces=64, slot_bytes=64 << 20) as pool:
+        for batch in (range(0, 4), range(4, 8), range(8, 12)):
+            for i in batch:
+                pool.spawn(i, 0, bytearray(pieces[i]), pl, want[i])
+            pool.flush()  # 2nd and 3rd: a batch is in flight -> deferred
+            for r in pool.try_iter():
+                got[r.index] = r
+        t0 = time.time()
+        while len(got) < 12 and time.time() - t0 < 30:
+            for r in pool.try_iter():  # vx_poll launches the deferred slot
+                got[r.index] = r
+            time.sleep(0.001)
+    assert sorted(got) == list(range(12))
+    assert all(got[i].hash_matched and got[i].digest == want[i] for i in got)

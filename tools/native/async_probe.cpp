@@ -1,0 +1,126 @@
+// async_probe.cpp — throughput of the async download path (vx_submit /
+// vx_flush / vx_poll) when completed pieces sit in scattered pool buffers.
+//
+// vortex hands each completed piece's pool buffer to the hasher
+// (peer_connection.rs:1145-1158); consecutive pieces come from unrelated
+// buffers of the BufferPool (buf_pool.rs:92-133).  This fills a pool of
+// `nbuf` buffers once, takes their digests with vx_sha1_batch, then submits
+// `total` pieces from a shuffled buffer order as fast as the engine takes
+// them, flushing every `flush_every` submits and polling like the event loop
+// (event_loop.rs:554-557).  Every completion must match.  Prints one JSON
+// line: GiB/s of piece bytes submitted → verdict polled.
+//
+// usage: async_probe <piece_len> [nbuf=1024] [total_GiB=8] [flush_every=64] [registered=1] [slot_MiB=default]
+#include <sys/mman.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <random>
+#include <vector>
+
+#include "vx_hash.h"
+
+static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        std::fprintf(stderr, "usage: %s piece_len [nbuf] [total_GiB] [flush_every] [registered]\n", argv[0]);
+        return 2;
+    }
+    const uint32_t plen = (uint32_t)std::strtoul(argv[1], nullptr, 0);
+    const uint32_t nbuf = argc > 2 ? (uint32_t)std::atoi(argv[2]) : 1024;
+    const double total_gib = argc > 3 ? std::atof(argv[3]) : 8.0;
+    const uint32_t flush_every = argc > 4 ? (uint32_t)std::atoi(argv[4]) : 64;
+    const bool registered = argc > 5 ? std::atoi(argv[5]) != 0 : true;
+    const uint64_t total = (uint64_t)(total_gib * (1ull << 30) / plen);
+
+    vx_config cfg;
+    vx_config_default(&cfg, plen);
+    if (argc > 6) {
+        cfg.slot_bytes = std::strtoull(argv[6], nullptr, 0) << 20;
+        cfg.batch_pieces = (uint32_t)std::min<uint64_t>(65536, cfg.slot_bytes / ((plen + 255) / 256 * 256));
+    }
+    vx_ctx* ctx = nullptr;
+    if (int rc = vx_create(&cfg, &ctx)) {
+        std::fprintf(stderr, "vx_create: %d %s\n", rc, vx_last_error());
+        return 1;
+    }
+    const size_t pool_bytes = (size_t)nbuf * plen;
+    uint8_t* pool = static_cast<uint8_t*>(
+        mmap(nullptr, pool_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_POPULATE, -1, 0));
+    if (pool == MAP_FAILED) return 1;
+    std::mt19937_64 rng(plen);
+    for (size_t i = 0; i < pool_bytes / 8; ++i) reinterpret_cast<uint64_t*>(pool)[i] = rng();
+    if (registered) {
+        if (int rc = vx_register_host_buffer(ctx, pool, pool_bytes)) {
+            std::fprintf(stderr, "register: %d %s\n", rc, vx_last_error());
+            return 1;
+        }
+    }
+    std::vector<const uint8_t*> ptrs(nbuf);
+    std::vector<uint32_t> lens(nbuf, plen);
+    for (uint32_t b = 0; b < nbuf; ++b) ptrs[b] = pool + (size_t)b * plen;
+    std::vector<uint8_t> digests((size_t)nbuf * 20);
+    if (int rc = vx_sha1_batch(ctx, ptrs.data(), lens.data(), nbuf, digests.data())) {
+        std::fprintf(stderr, "vx_sha1_batch: %d %s\n", rc, vx_last_error());
+        return 1;
+    }
+    std::vector<uint32_t> order(nbuf);
+    std::iota(order.begin(), order.end(), 0);
+    std::vector<vx_completion> cq(4096);
+    uint64_t polled = 0, bad = 0;
+    auto poll = [&]() -> int {
+        for (;;) {
+            const int64_t k = vx_poll(ctx, cq.data(), cq.size());
+            if (k < 0) return (int)k;
+            for (int64_t j = 0; j < k; ++j) bad += cq[j].matched ? 0 : 1;
+            polled += (uint64_t)k;
+            if ((size_t)k < cq.size()) return 0;
+        }
+    };
+    // warm-up: four passes over the pool with the timed flush cadence, so
+    // every slot has run (and allocated its pinned stage, if it needs one)
+    uint64_t sent = 0;
+    for (int pass = 0; pass < 4; ++pass) {
+        std::shuffle(order.begin(), order.end(), rng);
+        for (uint32_t b : order) {
+            if (vx_submit(ctx, b, ptrs[b], plen, &digests[(size_t)b * 20])) return 1;
+            if (++sent % flush_every == 0 && (vx_flush(ctx) || poll())) return 1;
+        }
+    }
+    if (vx_drain(ctx, 0) || poll()) return 1;
+    polled = 0;
+    bad = 0;
+    sent = 0;
+    const double t0 = now_s();
+    while (sent < total) {
+        std::shuffle(order.begin(), order.end(), rng);
+        for (uint32_t b : order) {
+            if (sent == total) break;
+            if (int rc = vx_submit(ctx, b, ptrs[b], plen, &digests[(size_t)b * 20])) {
+                std::fprintf(stderr, "vx_submit: %d %s\n", rc, vx_last_error());
+                return 1;
+            }
+            if (++sent % flush_every == 0) {
+                if (vx_flush(ctx) || poll()) return 1;
+            }
+        }
+    }
+    if (vx_drain(ctx, 0) || poll()) return 1;
+    const double el = now_s() - t0;
+    if (registered) vx_unregister_host_buffer(ctx, pool);
+    vx_destroy(ctx);
+    munmap(pool, pool_bytes);
+    std::printf("{\"piece_len\": %u, \"pieces\": %llu, \"registered\": %d, \"flush_every\": %u, \"GiBps\": %.3f, "
+                "\"mismatched\": %llu, \"polled\": %llu}\n",
+                plen, (unsigned long long)total, registered ? 1 : 0, flush_every,
+                (double)total * plen / el / (1 << 30), (unsigned long long)bad, (unsigned long long)polled);
+    return bad == 0 && polled == total ? 0 : 3;
+}

@@ -34,7 +34,7 @@ EXPORTS = (
     "vx_sha1_batch", "vx_verify_batch", "vx_verify_files", "vx_verify_files_range",
     "vx_sha1_device_uniform", "vx_sha1_device_ragged", "vx_sort_order",
     "vx_synth_fill", "vx_sha1_device_uniform_variant", "vx_sha1_device_ragged_variant",
-    "vx_tuning_chunk_rounds",
+    "vx_tuning_chunk_rounds", "vx_tuning_gather_tiles",
 )
 
 
@@ -90,6 +90,7 @@ def _declare(L: ctypes.CDLL) -> None:
                                            c.c_int),
         "vx_sha1_device_ragged_variant": ([vp, vp, vp, vp, c.c_uint32, vp, vp, vp, vp, c.c_int], c.c_int),
         "vx_tuning_chunk_rounds": ([vp], c.c_uint64),
+        "vx_tuning_gather_tiles": ([vp], c.c_uint64),
         "vx_synth_fill": ([vp, c.c_uint64, c.c_uint32, c.c_uint32, c.c_uint64, c.c_uint64, c.c_uint32, vp],
                           c.c_int),
     }

@@ -10,10 +10,10 @@
 // Design (DESIGN.md "Host engine"): a context owns `slots` batch slots, each
 // with its own HIP stream, a device arena, a pinned staging arena and pinned
 // metadata.  Pieces are appended to the filling slot at 256-byte aligned
-// offsets: pieces inside a registered (pinned) host range are DMA'd straight
-// from the caller's buffer at launch (adjacent pieces coalesced into one
-// copy); others are memcpy'd into the slot's pinned stage at submit and moved
-// with one H2D per contiguous run at launch.
+// offsets: pieces inside a registered (pinned) host range are pulled at launch
+// by one gather kernel through the range's device mapping (vx_gather.hip);
+// others are memcpy'd into the slot's pinned stage at submit and moved with
+// one H2D per contiguous run at launch.
 // A launch is H2D(meta) → kernel → D2H(digests, verdicts) → event; slots on
 // different streams overlap copy and compute.  vx_poll harvests finished
 // slots without blocking.  No internal threads: like the reference's loop,
@@ -95,6 +95,11 @@ struct Slot {
     uint64_t* d_poff = nullptr;
     uint64_t* h_tlen = nullptr;  // chunked re-verify: the piece's total length
     uint64_t* d_tlen = nullptr;
+    uint64_t* h_src = nullptr;   // gather: device-mapped source of piece i (0 = not gathered)
+    uint64_t* d_src = nullptr;
+    uint32_t* h_tfirst = nullptr;  // gather: piece i owns tiles [tfirst[i], tfirst[i+1])
+    uint32_t* d_tfirst = nullptr;
+    uint32_t gtiles = 0;           // gather tiles of this batch
     uint64_t* d_offsets = nullptr;
     uint32_t* d_lens = nullptr;
     uint8_t* d_expected = nullptr;
@@ -139,8 +144,18 @@ struct vx_ctx {
     uint8_t* d_table = nullptr;
     uint32_t n_table = 0;
     int filling = -1;
+    // vx_flush found every other slot in flight and left the filling slot
+    // open; vx_poll launches it once a slot frees.
+    bool flush_pending = false;
+    bool lazy_flush = true;  // VX_LAZY_FLUSH=0: flush always launches (A/B)
     std::deque<vx_completion> done;
-    std::map<uintptr_t, size_t> registered;
+    struct Reg {
+        size_t len;
+        uint8_t* dev;  // device mapping of the range (hipHostGetDevicePointer)
+    };
+    std::map<uintptr_t, Reg> registered;
+    bool gather = true;        // VX_GATHER=0 turns the gather kernel off (A/B)
+    uint64_t gather_tiles = 0;  // tiles gathered (vx_tuning_gather_tiles)
     uint64_t pending = 0;
     uint64_t seq = 0;
     int sticky = 0;
@@ -161,12 +176,16 @@ int set_device(const vx_ctx* c) {
     return 0;
 }
 
-bool is_registered(const vx_ctx* c, const void* p, size_t len) {
+// True if [p, p+len) lies in one registered range; *dev (optional) gets the
+// device-mapped address of p.
+bool is_registered(const vx_ctx* c, const void* p, size_t len, const uint8_t** dev = nullptr) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     auto it = c->registered.upper_bound(a);
     if (it == c->registered.begin()) return false;
     --it;
-    return a >= it->first && a + len <= it->first + it->second;
+    if (!(a >= it->first && a + len <= it->first + it->second.len)) return false;
+    if (dev) *dev = it->second.dev + (a - it->first);
+    return true;
 }
 
 int free_slot_mem(Slot& s) {
@@ -189,27 +208,51 @@ int alloc_slot(Slot& s, uint64_t arena, uint32_t cap) {
     VX_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
     VX_HIP(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
     if (hipMalloc(&s.d_arena, arena) != hipSuccess) return fail(VX_ENOMEM, "device arena allocation failed");
-    if (hipHostMalloc(&s.h_stage, arena, hipHostMallocDefault) != hipSuccess)
-        return fail(VX_ENOMEM, "pinned stage allocation failed");
-    const size_t meta = (size_t)cap * (8 + 4 + 4 + 20 + 20 + 8 + 8 + 1) + 64;
+    // The pinned stage is allocated on first use (ensure_stage): a caller that
+    // registers its buffer pool never stages, and pinning slot_bytes of host
+    // memory per slot up front would cost as much as the HBM arena.
+    // offsets | chunk offsets | total lens | gather sources | lens | piece rows |
+    // gather tile prefix (cap+1) | expected | digests | verdicts
+    const size_t meta = (size_t)cap * (8 + 8 + 8 + 8 + 4 + 4 + 4 + 20 + 20 + 1) + 64;
     if (hipHostMalloc(&s.h_meta, meta, hipHostMallocDefault) != hipSuccess)
         return fail(VX_ENOMEM, "pinned metadata allocation failed");
     if (hipMalloc(&s.d_meta, meta) != hipSuccess) return fail(VX_ENOMEM, "device metadata allocation failed");
-    // offsets | chunk offsets | total lens | lens | piece rows | expected | digests | verdicts
-    auto carve = [cap](uint8_t* b, uint64_t*& off, uint64_t*& poff, uint64_t*& tlen, uint32_t*& lens,
-                       uint32_t*& pidx, uint8_t*& exp, uint8_t*& dig, uint8_t*& m) {
-        off = reinterpret_cast<uint64_t*>(b);
-        poff = reinterpret_cast<uint64_t*>(b + (size_t)cap * 8);
-        tlen = reinterpret_cast<uint64_t*>(b + (size_t)cap * 16);
-        lens = reinterpret_cast<uint32_t*>(b + (size_t)cap * 24);
-        pidx = reinterpret_cast<uint32_t*>(b + (size_t)cap * 28);
-        exp = b + (size_t)cap * 32;
-        dig = b + (size_t)cap * 52;
-        m = b + (size_t)cap * 72;
+    auto carve = [cap](uint8_t* b, uint64_t*& off, uint64_t*& poff, uint64_t*& tlen, uint64_t*& src,
+                       uint32_t*& lens, uint32_t*& pidx, uint32_t*& tfirst, uint8_t*& exp, uint8_t*& dig,
+                       uint8_t*& m) {
+        size_t at = 0;
+        auto take = [&](size_t bytes) {
+            uint8_t* p = b + at;
+            at += bytes;
+            return p;
+        };
+        off = reinterpret_cast<uint64_t*>(take((size_t)cap * 8));
+        poff = reinterpret_cast<uint64_t*>(take((size_t)cap * 8));
+        tlen = reinterpret_cast<uint64_t*>(take((size_t)cap * 8));
+        src = reinterpret_cast<uint64_t*>(take((size_t)cap * 8));
+        lens = reinterpret_cast<uint32_t*>(take((size_t)cap * 4));
+        pidx = reinterpret_cast<uint32_t*>(take((size_t)cap * 4));
+        tfirst = reinterpret_cast<uint32_t*>(take((size_t)cap * 4 + 4));
+        exp = take((size_t)cap * 20);
+        dig = take((size_t)cap * 20);
+        m = take(cap);
     };
-    carve(s.h_meta, s.h_offsets, s.h_poff, s.h_tlen, s.h_lens, s.h_pidx, s.h_expected, s.h_digests, s.h_matched);
-    carve(s.d_meta, s.d_offsets, s.d_poff, s.d_tlen, s.d_lens, s.d_pidx, s.d_expected, s.d_digests, s.d_matched);
+    carve(s.h_meta, s.h_offsets, s.h_poff, s.h_tlen, s.h_src, s.h_lens, s.h_pidx, s.h_tfirst, s.h_expected,
+          s.h_digests, s.h_matched);
+    carve(s.d_meta, s.d_offsets, s.d_poff, s.d_tlen, s.d_src, s.d_lens, s.d_pidx, s.d_tfirst, s.d_expected,
+          s.d_digests, s.d_matched);
+    s.h_tfirst[0] = 0;
     s.tags.reserve(cap);
+    return 0;
+}
+
+// Pinned stage of slot s (unregistered pieces, file reads), allocated on first use.
+int ensure_stage(Slot& s) {
+    if (s.h_stage) return 0;
+    if (hipHostMalloc(&s.h_stage, s.arena_cap, hipHostMallocDefault) != hipSuccess) {
+        s.h_stage = nullptr;
+        return fail(VX_ENOMEM, "pinned stage allocation failed");
+    }
     return 0;
 }
 
@@ -219,6 +262,8 @@ void reset_fill(Slot& s) {
     s.druns.clear();
     s.n = 0;
     s.bytes = 0;
+    s.gtiles = 0;
+    if (s.h_tfirst) s.h_tfirst[0] = 0;
     s.uniform = true;
     s.has_expected = false;
     s.use_table = false;
@@ -270,7 +315,7 @@ int warm_slots(vx_ctx* c) {
         Slot& s = c->slots[si];
         hipStream_t st = s.stream;
         if (prev >= 0) VX_HIP(hipStreamWaitEvent(st, c->slots[prev].copied, 0));
-        VX_HIP(hipMemcpyAsync(s.d_arena, s.h_stage, std::min<uint64_t>(s.arena_cap, 8ull << 20),
+        VX_HIP(hipMemcpyAsync(s.d_arena, s.h_meta, std::min<uint64_t>(s.arena_cap, (uint64_t)s.cap * 85),
                               hipMemcpyHostToDevice, st));
         VX_HIP(hipMemcpyAsync(s.d_expected, s.h_expected, 20, hipMemcpyHostToDevice, st));
         VX_HIP(hipEventRecord(s.copied, st));
@@ -306,7 +351,10 @@ int launch_slot(vx_ctx* c, int si) {
 
 int launch_slot_impl(vx_ctx* c, int si) {
     Slot& s = c->slots[si];
-    if (c->filling == si) c->filling = -1;
+    if (c->filling == si) {
+        c->filling = -1;
+        c->flush_pending = false;
+    }
     if (s.n == 0) {
         s.state = Slot::FREE;
         return 0;
@@ -318,16 +366,23 @@ int launch_slot_impl(vx_ctx* c, int si) {
     for (const Run& r : s.runs)
         VX_HIP(hipMemcpyAsync(s.d_arena + r.lo, s.h_stage + r.lo, r.hi - r.lo, hipMemcpyHostToDevice, cs));
     const uint32_t n = s.n;
+    if (!s.uniform || s.gtiles) {
+        VX_HIP(hipMemcpyAsync(s.d_offsets, s.h_offsets, (size_t)n * 8, hipMemcpyHostToDevice, cs));
+        VX_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)n * 4, hipMemcpyHostToDevice, cs));
+    }
+    if (s.gtiles) {
+        VX_HIP(hipMemcpyAsync(s.d_src, s.h_src, (size_t)n * 8, hipMemcpyHostToDevice, cs));
+        VX_HIP(hipMemcpyAsync(s.d_tfirst, s.h_tfirst, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, cs));
+        hipError_t e = vx::launch_gather(s.d_src, s.d_offsets, s.d_lens, s.d_tfirst, n, s.gtiles, s.d_arena, cs);
+        if (e != hipSuccess) return hip_fail(e, "gather launch");
+        c->gather_tiles += s.gtiles;
+    }
     if (s.use_table)
         VX_HIP(hipMemcpyAsync(s.d_pidx, s.h_pidx, (size_t)n * 4, hipMemcpyHostToDevice, cs));
     else if (s.has_expected)
         VX_HIP(hipMemcpyAsync(s.d_expected, s.h_expected, (size_t)n * 20, hipMemcpyHostToDevice, cs));
     const uint8_t* d_exp = s.use_table ? c->d_table : (s.has_expected ? s.d_expected : nullptr);
     const uint32_t* d_row = s.use_table ? s.d_pidx : nullptr;
-    if (!s.uniform) {
-        VX_HIP(hipMemcpyAsync(s.d_offsets, s.h_offsets, (size_t)n * 8, hipMemcpyHostToDevice, cs));
-        VX_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)n * 4, hipMemcpyHostToDevice, cs));
-    }
     VX_HIP(hipEventRecord(s.copied, cs));
     if (cs != s.stream) VX_HIP(hipStreamWaitEvent(s.stream, s.copied, 0));
     mark_launched(c, si);
@@ -384,6 +439,14 @@ int reap(vx_ctx* c, bool block_oldest) {
     return 0;
 }
 
+// A flush may launch now if, after it, a slot is still free to fill (with a
+// single slot: if nothing is in flight).
+bool may_launch_now(const vx_ctx* c) {
+    int inflight = 0;
+    for (const Slot& s : c->slots) inflight += s.state == Slot::INFLIGHT;
+    return inflight < std::max(1, (int)c->slots.size() - 1);
+}
+
 int acquire_filling(vx_ctx* c) {
     if (c->filling >= 0) return c->filling;
     for (;;) {
@@ -422,7 +485,14 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
         off = 0;
     }
     const uint32_t i = s->n;
-    if (len) {
+    const uint8_t* dev = nullptr;
+    s->h_src[i] = 0;
+    if (len && c->gather && (reinterpret_cast<uintptr_t>(data) & 15) == 0 && is_registered(c, data, len, &dev)) {
+        // Registered, 16-byte aligned: the launch's gather kernel pulls it
+        // through the range's device mapping.
+        s->h_src[i] = reinterpret_cast<uint64_t>(dev);
+        s->gtiles += vx::gather_tiles(len);
+    } else if (len) {
         if (is_registered(c, data, len)) {
             // Pinned source: DMA straight from the caller's buffer at launch;
             // pieces adjacent in host memory AND in the arena share one copy.
@@ -432,6 +502,7 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
             else
                 s->druns.push_back(DirectRun{data, off, off + len});
         } else {
+            if (int rc = ensure_stage(*s)) return rc;
             std::memcpy(s->h_stage + off, data, len);
             if (!s->runs.empty() && s->runs.back().hi == off)
                 s->runs.back().hi = off + len;
@@ -443,6 +514,7 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
     }
     s->h_offsets[i] = off;
     s->h_lens[i] = len;
+    s->h_tfirst[i + 1] = s->gtiles;
     // Equal lengths at 256-byte aligned back-to-back offsets are a uniform
     // batch: offset(i) = i * align_up(len, 256) (the uniform kernel's layout).
     if (i > 0 && len != s->h_lens[0]) s->uniform = false;
@@ -501,7 +573,14 @@ void vx_config_default(vx_config* cfg, uint32_t max_piece_len) {
     cfg->device = 0;
     cfg->max_piece_len = max_piece_len;
     cfg->slots = 4;
-    cfg->slot_bytes = std::max<uint64_t>(128ull << 20, align_up(max_piece_len, kAlign) * 16);
+    // Throughput of the async path is bytes in flight / batch latency, and a
+    // batch's latency is its longest piece's chain (~28 ms at 2 MiB), so slots
+    // grow with the piece length: 128 pieces each, 128 MiB to 2 GiB of HBM.
+    // (The pinned stage is only allocated for unregistered pieces; keeping it
+    // at 128 MiB for short pieces keeps their staging memcpy cache-friendly:
+    // 256 MiB slots halved the unregistered 16 KiB rate, async_probe.)
+    const uint64_t piece = align_up(std::max<uint32_t>(max_piece_len, 1), kAlign);
+    cfg->slot_bytes = std::max(piece, std::min<uint64_t>(2ull << 30, std::max<uint64_t>(128ull << 20, piece * 128)));
     cfg->batch_pieces = (uint32_t)std::min<uint64_t>(65536, cfg->slot_bytes / align_up(std::max<uint32_t>(max_piece_len, 1), kAlign));
 }
 
@@ -517,6 +596,8 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (!c) return fail(VX_ENOMEM, "vx_create: out of host memory");
     c->cfg = *cfg;
     if (const char* m = std::getenv("VX_H2D_MODE")) c->h2d_mode = std::atoi(m) & 3;
+    if (const char* m = std::getenv("VX_GATHER")) c->gather = std::atoi(m) != 0;
+    if (const char* m = std::getenv("VX_LAZY_FLUSH")) c->lazy_flush = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_BATCH_CHUNK")) c->batch_chunk = align_up(std::strtoull(m, nullptr, 0), kAlign);
     int rc = set_device(c);
     if (!rc && c->h2d_mode == 3 && hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess)
@@ -560,12 +641,17 @@ int vx_register_host_buffer(vx_ctx* c, void* ptr, size_t len) {
     if (it != c->registered.end() && it->first < a + len) return fail(VX_EINVAL, "overlapping registration");
     if (it != c->registered.begin()) {
         auto p = std::prev(it);
-        if (p->first + p->second > a) return fail(VX_EINVAL, "overlapping registration");
+        if (p->first + p->second.len > a) return fail(VX_EINVAL, "overlapping registration");
     }
     int rc = set_device(c);
     if (rc) return rc;
-    VX_HIP(hipHostRegister(ptr, len, hipHostRegisterDefault));
-    c->registered[a] = len;
+    VX_HIP(hipHostRegister(ptr, len, hipHostRegisterMapped));
+    void* dev = nullptr;
+    if (hipHostGetDevicePointer(&dev, ptr, 0) != hipSuccess || !dev) {
+        (void)hipHostUnregister(ptr);
+        return fail(VX_EDEVICE, "vx_register_host_buffer: no device mapping");
+    }
+    c->registered[a] = vx_ctx::Reg{len, static_cast<uint8_t*>(dev)};
     return 0;
 }
 
@@ -612,12 +698,24 @@ int vx_submit_piece(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, 
     return submit_impl(c, tag, data, len, nullptr, (int64_t)piece_index);
 }
 
+// Launch the filling slot unless that would leave no slot free for the next
+// submit: then the slot stays open and keeps collecting pieces, and vx_poll
+// launches it as soon as a batch completes.  So under load batches grow
+// instead of the event-loop thread blocking in vx_submit for a whole batch
+// (DESIGN.md §6.5).
 int vx_flush(vx_ctx* c) {
     if (!c) return fail(VX_EINVAL, "vx_flush: NULL context");
     if (c->sticky) return c->sticky;
-    if (c->filling < 0) return 0;
+    if (c->filling < 0 || c->slots[c->filling].n == 0) return 0;
     int rc = set_device(c);
     if (rc) return rc;
+    if (c->lazy_flush) {
+        if ((rc = reap(c, false))) return rc;
+        if (!may_launch_now(c)) {
+            c->flush_pending = true;
+            return 0;
+        }
+    }
     return launch_slot(c, c->filling);
 }
 
@@ -628,6 +726,7 @@ int64_t vx_poll(vx_ctx* c, vx_completion* out, size_t max) {
     if (rc) return rc;
     rc = reap(c, false);
     if (rc) return rc;
+    if (c->flush_pending && c->filling >= 0 && may_launch_now(c) && (rc = launch_slot(c, c->filling))) return rc;
     size_t k = 0;
     while (k < max && !c->done.empty()) {
         out[k++] = c->done.front();
@@ -639,8 +738,10 @@ int64_t vx_poll(vx_ctx* c, vx_completion* out, size_t max) {
 
 int vx_drain(vx_ctx* c, uint32_t timeout_ms) {
     if (!c) return fail(VX_EINVAL, "vx_drain: NULL context");
-    int rc = vx_flush(c);
+    if (c->sticky) return c->sticky;
+    int rc = set_device(c);
     if (rc) return rc;
+    if (c->filling >= 0 && (rc = launch_slot(c, c->filling))) return rc;  // forced, unlike vx_flush
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
         bool any = false;
@@ -716,6 +817,7 @@ int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl,
         if (si < 0) return si;
         Slot& s = c->slots[si];
         reset_fill(s);
+        if ((rc = ensure_stage(s))) return rc;
         const uint64_t cap = std::min<uint64_t>(s.cap, std::max<uint64_t>(1, s.arena_cap / stride));
         const uint64_t lo = next, hi = std::min<uint64_t>(end, next + cap);
         items.clear();
@@ -887,6 +989,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
             }
             Slot& s = c->slots[si];
             reset_fill(s);
+            if ((rc = ensure_stage(s))) break;
             items.clear();
             uint32_t m = 0;
             for (uint64_t i = w0; i < w1; ++i) {
@@ -1173,6 +1276,7 @@ int vx_sha1_device_ragged(const void* d_base, const uint64_t* d_offsets, const u
 }
 
 uint64_t vx_tuning_chunk_rounds(const vx_ctx* c) { return c ? c->chunk_rounds : 0; }
+uint64_t vx_tuning_gather_tiles(const vx_ctx* c) { return c ? c->gather_tiles : 0; }
 
 int vx_sort_order(const uint32_t* lens, uint32_t n, uint32_t* order_out) {
     if (n && (!lens || !order_out)) return fail(VX_EINVAL, "vx_sort_order: NULL argument");

@@ -129,11 +129,19 @@ class Readers {
         cv_.notify_all();
         for (auto& t : th_) t.join();
     }
+    // The caller may rebuild `items` as soon as run() returns, so a worker
+    // takes an item only under the lock and only while the generation it woke
+    // for is still the current one: main waits in run() until every taken
+    // item is done, so the vector is stable while any worker reads it.  (A
+    // lock-free counter let a worker that woke late for a finished
+    // generation index the vector while the caller was refilling it.)
     void run(const std::vector<ReadItem>& items) {
+        if (items.empty()) return;
         {
             std::lock_guard<std::mutex> g(mu_);
             items_ = &items;
-            next_.store(0);
+            next_ = 0;
+            count_ = items.size();
             left_ = items.size();
             ++gen_;
         }
@@ -147,25 +155,23 @@ class Readers {
         std::vector<Seg> segs;
         uint64_t seen = 0;
         for (;;) {
-            const std::vector<ReadItem>* items;
             {
                 std::unique_lock<std::mutex> g(mu_);
                 cv_.wait(g, [&] { return stop_ || gen_ != seen; });
                 if (stop_) return;
                 seen = gen_;
-                items = items_;
             }
-            uint64_t mine = 0;
             for (;;) {
-                const uint64_t k = next_.fetch_add(1);
-                if (k >= items->size()) break;
-                const ReadItem& it = (*items)[k];
-                if (!read_range(fs_, fds_, pl_, it, segs)) bad_[it.piece - first_] = 1;
-                ++mine;
+                const ReadItem* it;
+                {
+                    std::lock_guard<std::mutex> g(mu_);
+                    if (gen_ != seen || next_ >= count_) break;  // never touches a finished vector
+                    it = &(*items_)[next_++];
+                }
+                if (!read_range(fs_, fds_, pl_, *it, segs)) bad_[it->piece - first_] = 1;
+                std::lock_guard<std::mutex> g(mu_);
+                if (--left_ == 0) done_cv_.notify_all();
             }
-            std::lock_guard<std::mutex> g(mu_);
-            left_ -= mine;
-            if (left_ == 0) done_cv_.notify_all();
         }
     }
 
@@ -180,7 +186,7 @@ class Readers {
     bool stop_ = false;
     uint64_t gen_ = 0, left_ = 0;
     const std::vector<ReadItem>* items_ = nullptr;
-    std::atomic<uint64_t> next_{0};
+    uint64_t next_ = 0, count_ = 0;
 };
 
 }  // namespace vx_files

@@ -45,6 +45,14 @@ hipError_t launch_chunk(const uint8_t* base, const uint64_t* offsets, const uint
                         const uint32_t* pids, const uint64_t* poffs, const uint64_t* tlens, uint32_t* states,
                         uint8_t* digests, const uint8_t* expected, uint8_t* matched, hipStream_t stream);
 
+// Gather registered host pieces into a slot arena (vx_gather.hip, DESIGN.md
+// §6.5): piece i (16-byte aligned device-mapped source src[i], length
+// lens[i]) lands at arena + dst_off[i]; it owns 64 KiB tiles
+// [tfirst[i], tfirst[i+1]) of the ntiles = tfirst[n] total.
+uint32_t gather_tiles(uint32_t len);
+hipError_t launch_gather(const uint64_t* src, const uint64_t* dst_off, const uint32_t* lens, const uint32_t* tfirst,
+                         uint32_t n, uint32_t ntiles, uint8_t* arena, hipStream_t stream);
+
 hipError_t launch_synth_fill(uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint64_t first,
                              uint64_t seed, uint32_t corrupt_every, hipStream_t stream);
 
