@@ -100,8 +100,9 @@ int vx_create(const vx_config* cfg, vx_ctx** out);
  * hash before EventLoop::run returns, event_loop.rs:385-602), then frees. */
 int vx_destroy(vx_ctx* ctx);
 
-/* Pin a host range (e.g. a BufferPool's AnonymousMmap, buf_ring.rs:24-42) so
- * pieces inside it are DMA'd straight to the GPU instead of being staged
+/* Pin and device-map a host range (e.g. a BufferPool's AnonymousMmap,
+ * buf_ring.rs:24-42) so pieces inside it are pulled straight to the GPU (one
+ * gather kernel per batch reads them over PCIe) instead of being staged
  * through an internal pinned copy.  Ranges must not overlap. */
 int vx_register_host_buffer(vx_ctx* ctx, void* ptr, size_t len);
 int vx_unregister_host_buffer(vx_ctx* ctx, void* ptr);
@@ -123,7 +124,10 @@ int vx_set_piece_table(vx_ctx* ctx, const uint8_t* table, uint32_t n_pieces);
 /* vx_submit with expected = row piece_index of the piece table. */
 int vx_submit_piece(vx_ctx* ctx, uint64_t tag, const uint8_t* data, uint32_t len, uint32_t piece_index);
 /* Launch whatever is queued (call once per event-loop turn, next to the
- * drain at event_loop.rs:554-557). */
+ * drain at event_loop.rs:554-557).  If launching would leave no batch slot
+ * free for the next vx_submit, the queued pieces stay open and keep
+ * collecting, and the next vx_poll launches them once a batch completes:
+ * under load batches grow instead of vx_submit blocking the loop thread. */
 int vx_flush(vx_ctx* ctx);
 /* Replaces `downloaded_piece_rc.try_recv()` (torrent.rs:418): non-blocking,
  * returns how many completions were written to out[0..max).  Order is the
