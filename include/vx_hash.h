@@ -181,11 +181,17 @@ int vx_sha1_device_uniform(const void* d_base, uint64_t stride, uint32_t len, ui
 /* Ragged batch: piece i at d_base + d_offsets[i] (16-byte aligned), d_lens[i]
  * bytes.  d_order (may be NULL) is a permutation of [0,n) telling lane j to
  * hash piece d_order[j]; pass pieces sorted by descending length so each
- * wavefront gets equal-length work (see vx_sort_order).  max_len bounds all
- * lengths (used only to validate). */
+ * wavefront gets equal-length work (see vx_sort_order).  Runs the kernel
+ * suited to chain-bound batches (lengths that differ). */
 int vx_sha1_device_ragged(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
                           const uint32_t* d_order, uint32_t n, void* d_digests, const void* d_expected,
                           void* d_matched, void* stream);
+/* As vx_sha1_device_ragged, with the batch's longest piece and total bytes
+ * (known on the host when the batch is laid out) so the engine picks the
+ * kernel whose time bound, throughput or longest chain, is lower. */
+int vx_sha1_device_ragged_hint(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
+                               const uint32_t* d_order, uint32_t n, uint32_t max_len, uint64_t total_len,
+                               void* d_digests, const void* d_expected, void* d_matched, void* stream);
 /* Host helper: write into order_out the permutation that sorts lens[0..n)
  * by descending length (stable).  Used to build d_order. */
 int vx_sort_order(const uint32_t* lens, uint32_t n, uint32_t* order_out);

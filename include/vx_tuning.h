@@ -24,6 +24,10 @@ uint64_t vx_tuning_chunk_rounds(const struct vx_ctx* ctx);
 /* 64 KiB tiles the context's gather kernel has pulled from registered host
  * buffers (async / batch slots). */
 uint64_t vx_tuning_gather_tiles(const struct vx_ctx* ctx);
+/* The kernel vx_sha1_device_ragged_hint runs for a batch of n pieces whose
+ * longest is max_len bytes, total_len bytes in all: 1 = lane, 2 = split
+ * (host-only). */
+int vx_tuning_plan_ragged(uint32_t n, uint32_t max_len, uint64_t total_len);
 
 int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
                                    const void* d_expected, void* d_matched, void* stream, int variant);

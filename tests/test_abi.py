@@ -105,3 +105,21 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(ImportError):
         _lib.lib()
+
+
+def test_ragged_plan_host(built):
+    """The ragged kernel planner on the BASELINE geometries:
+    throughput-bound batches of equal pieces go to the lane kernel, batches
+    bound by their longest chain (config 3's 4 MiB pieces, config 5's 2 MiB
+    pieces, small batches) to the split kernel."""
+    from vortex_amd import _lib
+
+    plan = _lib.lib().vx_tuning_plan_ragged
+    LANE, SPLIT = 1, 2
+    KiB, MiB = 1024, 1 << 20
+    assert plan(65536, 256 * KiB, 65536 * 256 * KiB) == LANE                     # config 2 as a ragged batch
+    c3 = 262144 * 16 * KiB + 16384 * 256 * KiB + 4096 * MiB + 1024 * 4 * MiB      # config 3, 16 GiB
+    assert plan(262144 + 16384 + 4096 + 1024, 4 * MiB, c3) == SPLIT
+    assert plan(1387, 2 * MiB, 2907832320) == SPLIT                                # config 5 geometry
+    assert plan(16384, 256 * KiB, 16384 * 256 * KiB) == SPLIT                      # chip not full
+    assert plan(1 << 20, 16 * KiB, (1 << 20) * 16 * KiB) == LANE                   # many short pieces

@@ -259,7 +259,8 @@ def test_config3_ragged_full(built, gpu):
     perm = np.random.default_rng(0x5EED0003).permutation(len(offs))
     offs, lens, cls = offs[perm], lens[perm], cls[perm]
     order = vdev.length_order(lens).to(gpu)
-    dig, _ = vdev.sha1_ragged(data, torch.from_numpy(offs).to(gpu), torch.from_numpy(lens).to(gpu), order=order)
+    dig, _ = vdev.sha1_ragged(data, torch.from_numpy(offs).to(gpu), torch.from_numpy(lens).to(gpu), order=order,
+                              plan=vdev.ragged_plan(lens))  # planned default (split: chain-bound)
     torch.cuda.synchronize()
     got = dig.cpu().numpy()
     del data

@@ -2,8 +2,9 @@
 """Device-resident ragged batches: BASELINE config 3 (16 KiB / 256 KiB / 1 MiB /
 4 MiB, 4 GiB each, shuffled, longest-first lane order) and the config-5
 geometry (1,387 x 2 MiB, last 1,179,648 B).  A/B of the ragged kernel
-variants (1 = lane, 2 = split) interleaved in one process; digests of the
-variants must agree.
+variants (1 = lane, 2 = split, 0 = the default kernel planned from the host
+lengths, vx_sha1_device_ragged_hint) interleaved in one process; digests of
+the variants must agree.
 
 usage: python tools/ragged_bench.py [--scale 1.0] [--rounds 3]
 """
@@ -36,7 +37,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="1,2")
+    ap.add_argument("--variants", default="1,2,0", help="1 lane, 2 split, 0 default planned from host lengths")
     a = ap.parse_args()
     import torch
 
@@ -67,13 +68,15 @@ def main():
         order = vdev.length_order(lens).to(dev)
         ref = None
         variants = [int(v) for v in a.variants.split(",")]
-        names = {1: "lane", 2: "split", 11: "split_opaque"}
+        names = {0: "default_planned", 1: "lane", 2: "split", 11: "split_opaque"}
+        plan = vdev.ragged_plan(lens)
         times = {v: [] for v in variants}
         for r in range(a.rounds + 1):
             for v in variants:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                dig, _ = vdev.sha1_ragged(data, d_off, d_len, order=order, variant=v)
+                dig, _ = vdev.sha1_ragged(data, d_off, d_len, order=order, variant=v,
+                                          plan=plan if v == 0 else None)
                 e1.record()
                 torch.cuda.synchronize()
                 if ref is None:

@@ -32,9 +32,9 @@ EXPORTS = (
     "vx_create", "vx_destroy", "vx_register_host_buffer", "vx_unregister_host_buffer",
     "vx_submit", "vx_flush", "vx_poll", "vx_drain", "vx_pending", "vx_set_piece_table", "vx_submit_piece",
     "vx_sha1_batch", "vx_verify_batch", "vx_verify_files", "vx_verify_files_range",
-    "vx_sha1_device_uniform", "vx_sha1_device_ragged", "vx_sort_order",
+    "vx_sha1_device_uniform", "vx_sha1_device_ragged", "vx_sha1_device_ragged_hint", "vx_sort_order",
     "vx_synth_fill", "vx_sha1_device_uniform_variant", "vx_sha1_device_ragged_variant",
-    "vx_tuning_chunk_rounds", "vx_tuning_gather_tiles",
+    "vx_tuning_chunk_rounds", "vx_tuning_gather_tiles", "vx_tuning_plan_ragged",
 )
 
 
@@ -85,12 +85,15 @@ def _declare(L: ctypes.CDLL) -> None:
                                    c.c_uint32], c.c_int64),
         "vx_sha1_device_uniform": ([vp, c.c_uint64, c.c_uint32, c.c_uint32, vp, vp, vp, vp], c.c_int),
         "vx_sha1_device_ragged": ([vp, vp, vp, vp, c.c_uint32, vp, vp, vp, vp], c.c_int),
+        "vx_sha1_device_ragged_hint": ([vp, vp, vp, vp, c.c_uint32, c.c_uint32, c.c_uint64, vp, vp, vp, vp],
+                                       c.c_int),
         "vx_sort_order": ([vp, c.c_uint32, vp], c.c_int),
         "vx_sha1_device_uniform_variant": ([vp, c.c_uint64, c.c_uint32, c.c_uint32, vp, vp, vp, vp, c.c_int],
                                            c.c_int),
         "vx_sha1_device_ragged_variant": ([vp, vp, vp, vp, c.c_uint32, vp, vp, vp, vp, c.c_int], c.c_int),
         "vx_tuning_chunk_rounds": ([vp], c.c_uint64),
         "vx_tuning_gather_tiles": ([vp], c.c_uint64),
+        "vx_tuning_plan_ragged": ([c.c_uint32, c.c_uint32, c.c_uint64], c.c_int),
         "vx_synth_fill": ([vp, c.c_uint64, c.c_uint32, c.c_uint32, c.c_uint64, c.c_uint64, c.c_uint32, vp],
                           c.c_int),
     }

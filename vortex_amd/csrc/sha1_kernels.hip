@@ -19,6 +19,8 @@
 //  * output: 20-byte big-endian digest per piece and, when an expected table
 //    is given, a 0/1 verdict byte (DownloadedPiece::hash_matched).
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "sha1_device.hpp"
@@ -649,14 +651,31 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, ui
 }  // namespace vx
 
 namespace vx {
+// Kernel choice for a ragged batch from its longest piece and total bytes
+// (DESIGN.md §3.4).  Each kernel's time is bounded below by its throughput
+// over all bytes and by the longest piece's chain, whichever is larger:
+//   lane : max(total / 3.4 TB/s, blocks(max_len) x 1.18 us)
+//   split: max(total / 2.5 TB/s, blocks(max_len) x 0.87 us)
+// (config 2 and config 3 measurements, §3.5: the lane kernel's VALU-bound
+// rate and per-block chain, the split kernel's).  Config 3's 4 MiB pieces make
+// it chain-bound: 77 ms lane vs 57 ms split, though it has 283,648 pieces.
+int plan_ragged(uint32_t n, uint64_t max_len, uint64_t total_len) {
+    (void)n;
+    const double blocks = (double)((max_len + 9 + 63) / 64);
+    const double lane = std::max((double)total_len / 3.4e12, blocks * 1.18e-6);
+    const double split = std::max((double)total_len / 2.5e12, blocks * 0.87e-6);
+    return lane < split ? kUniformLane : kUniformSplit;
+}
+
+// variant 0 without a plan: the split kernel.  A batch whose lengths really
+// differ is usually bound by its longest chain, where split's shorter per-block
+// chain wins by up to 2.3x; the lane kernel is at most 1.4x faster, and only on
+// throughput-bound batches of near-equal pieces (use the uniform entry, or
+// vx_sha1_device_ragged_hint, for those).
 hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens, const uint32_t* order,
                          uint32_t n, uint8_t* digests, const uint8_t* expected, uint8_t* matched,
                          hipStream_t stream, int variant, const uint32_t* exp_index) {
     if (variant == kUniformLane) return launch_ragged_lane(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
-    if (variant == kUniformSplit)
-        return launch_ragged_split(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
-    if (n <= kSplitMaxPieces)
-        return launch_ragged_split(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
-    return launch_ragged_lane(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
+    return launch_ragged_split(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
 }
 }  // namespace vx

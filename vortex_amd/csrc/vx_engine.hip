@@ -393,8 +393,13 @@ int launch_slot_impl(vx_ctx* c, int si) {
         e = vx::launch_uniform(s.d_arena, stride, len, n, s.d_digests, d_exp, s.d_matched, s.stream,
                                vx::kUniformDefault, d_row);
     } else {
+        uint64_t max_len = 0, total = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            max_len = std::max<uint64_t>(max_len, s.h_lens[i]);
+            total += s.h_lens[i];
+        }
         e = vx::launch_ragged(s.d_arena, s.d_offsets, s.d_lens, nullptr, n, s.d_digests, d_exp, s.d_matched,
-                              s.stream, vx::kUniformDefault, d_row);
+                              s.stream, vx::plan_ragged(n, max_len, total), d_row);
     }
     if (e != hipSuccess) return hip_fail(e, "kernel launch");
     VX_HIP(hipMemcpyAsync(s.h_digests, s.d_digests, (size_t)n * 20, hipMemcpyDeviceToHost, s.stream));
@@ -1275,8 +1280,18 @@ int vx_sha1_device_ragged(const void* d_base, const uint64_t* d_offsets, const u
                                          stream, 0);
 }
 
+int vx_sha1_device_ragged_hint(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
+                               const uint32_t* d_order, uint32_t n, uint32_t max_len, uint64_t total_len,
+                               void* d_digests, const void* d_expected, void* d_matched, void* stream) {
+    return vx_sha1_device_ragged_variant(d_base, d_offsets, d_lens, d_order, n, d_digests, d_expected, d_matched,
+                                         stream, vx::plan_ragged(n, max_len, total_len));
+}
+
 uint64_t vx_tuning_chunk_rounds(const vx_ctx* c) { return c ? c->chunk_rounds : 0; }
 uint64_t vx_tuning_gather_tiles(const vx_ctx* c) { return c ? c->gather_tiles : 0; }
+int vx_tuning_plan_ragged(uint32_t n, uint32_t max_len, uint64_t total_len) {
+    return vx::plan_ragged(n, max_len, total_len);
+}
 
 int vx_sort_order(const uint32_t* lens, uint32_t n, uint32_t* order_out) {
     if (n && (!lens || !order_out)) return fail(VX_EINVAL, "vx_sort_order: NULL argument");

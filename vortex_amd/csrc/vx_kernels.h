@@ -26,6 +26,10 @@ hipError_t launch_uniform_split(const uint8_t* base, uint64_t stride, uint32_t l
                                 const uint8_t* expected, uint8_t* matched, hipStream_t stream,
                                 const uint32_t* exp_index = nullptr);
 
+// Lane (kUniformLane) or split (kUniformSplit) for a ragged batch, from its
+// longest piece and total bytes.
+int plan_ragged(uint32_t n, uint64_t max_len, uint64_t total_len);
+
 hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens, const uint32_t* order,
                          uint32_t n, uint8_t* digests, const uint8_t* expected, uint8_t* matched,
                          hipStream_t stream, int variant = 0,

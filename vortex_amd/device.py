@@ -66,12 +66,16 @@ def sha1_uniform(data: torch.Tensor, n: int, piece_len: int, stride: Optional[in
 def sha1_ragged(data: torch.Tensor, offsets: torch.Tensor, lens: torch.Tensor,
                 order: Optional[torch.Tensor] = None, expected: Optional[torch.Tensor] = None,
                 digests: Optional[torch.Tensor] = None, matched: Optional[torch.Tensor] = None,
-                stream: Optional[torch.cuda.Stream] = None, variant: int = 0):
+                stream: Optional[torch.cuda.Stream] = None, variant: int = 0, plan=None):
     """Hash piece i = data[offsets[i] : offsets[i]+lens[i]] for all i.
 
     offsets: int64 device tensor (16-byte aligned values); lens: int32 device
     tensor; order: optional int32 permutation (see :func:`length_order`).
-    variant: 0 = default kernel; 1 lane / 2 split pin one (vx_tuning.h)."""
+    variant: 0 = default kernel; 1 lane / 2 split pin one (vx_tuning.h).
+    plan: (max_len, total_bytes) of the batch, known on the host when it is
+    laid out (see :func:`ragged_plan`); with variant 0 the engine then picks
+    the kernel whose time bound is lower (vx_sha1_device_ragged_hint,
+    DESIGN.md §3.4)."""
     _req(data, "data")
     _req(offsets, "offsets", torch.int64)
     _req(lens, "lens", torch.int32)
@@ -87,14 +91,28 @@ def sha1_ragged(data: torch.Tensor, offsets: torch.Tensor, lens: torch.Tensor,
             matched = torch.empty((n,), dtype=torch.uint8, device=dev)
     if order is not None:
         _req(order, "order", torch.int32)
-    rc = lib().vx_sha1_device_ragged_variant(
-        data.data_ptr(), offsets.data_ptr(), lens.data_ptr(),
-        order.data_ptr() if order is not None else None, n, digests.data_ptr(),
-        expected.data_ptr() if expected is not None else None,
-        matched.data_ptr() if expected is not None else None,
-        _stream_ptr(stream, dev), variant)
+    exp_p = expected.data_ptr() if expected is not None else None
+    m_p = matched.data_ptr() if expected is not None else None
+    order_p = order.data_ptr() if order is not None else None
+    if variant == 0 and plan is not None:
+        max_len, total = plan
+        rc = lib().vx_sha1_device_ragged_hint(data.data_ptr(), offsets.data_ptr(), lens.data_ptr(), order_p, n,
+                                              int(max_len), int(total), digests.data_ptr(), exp_p, m_p,
+                                              _stream_ptr(stream, dev))
+    else:
+        rc = lib().vx_sha1_device_ragged_variant(data.data_ptr(), offsets.data_ptr(), lens.data_ptr(), order_p, n,
+                                                 digests.data_ptr(), exp_p, m_p, _stream_ptr(stream, dev), variant)
     check(rc, "vx_sha1_device_ragged")
     return digests, matched
+
+
+def ragged_plan(lens_host) -> tuple[int, int]:
+    """(longest piece, total bytes) of a ragged batch: the `plan` argument of
+    :func:`sha1_ragged`."""
+    import numpy as np
+
+    arr = np.asarray(lens_host, dtype=np.uint64)
+    return (int(arr.max()) if arr.size else 0), int(arr.sum())
 
 
 def length_order(lens_host) -> torch.Tensor:
