@@ -4,7 +4,8 @@
  * (best measured) variant; this entry point lets tools/ and tests pin one.
  *   0 = default, 1 = lane-per-piece (one wave per 64 pieces does loads,
  *   schedule and rounds), 2 = producer/consumer split (a load+schedule wave
- *   feeds a rounds-only wave through an LDS ring).
+ *   feeds a rounds-only wave through an LDS ring), 3 / 4 = split with a 2- / 3-slot
+ *   LDS ring (A/B of the ring protocol; 2 uses the default ring).
  */
 #ifndef VX_TUNING_H
 #define VX_TUNING_H

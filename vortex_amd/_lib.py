@@ -15,7 +15,10 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libvortex_amd.so")
+# VX_LIB_OVERRIDE: A/B tooling only (tools/gpu_ab_builds.sh runs two builds of
+# the engine on one box, alternating processes); the product loads the in-tree
+# build.
+LIB_PATH = os.environ.get("VX_LIB_OVERRIDE") or os.path.join(_HERE, "libvortex_amd.so")
 
 VX_OK = 0
 VX_EINVAL = -22

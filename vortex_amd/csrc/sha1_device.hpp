@@ -28,6 +28,12 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) {
 #define VX_CH(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0xCA)
 #define VX_PAR(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0x96)
 #define VX_MAJ(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0xE8)
+// a ^ b as an 8-byte VOP3 v_bitop3_b32 (same issue cost as the 4-byte VOP2
+// v_xor_b32).  The message schedule's xor is the only 4-byte VALU op in the
+// hot loops; as VOP2 it flipped the 8-byte alignment of every instruction
+// after it, so ~1 in 4 of them straddled a 32-byte fetch boundary, and on
+// gfx950 each straddle cost about one issue slot.
+#define VX_XOR2(a, b) __builtin_amdgcn_bitop3_b32((a), (b), (b), 0x3C)
 
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
@@ -49,7 +55,7 @@ __device__ __forceinline__ void compress(State& s, uint32_t (&w)[16]) {
         if (t < 16) {
             wt = w[t];
         } else {
-            wt = rotl(VX_PAR(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
+            wt = rotl(VX_XOR2(VX_PAR(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]), w[t & 15]), 1);
             w[t & 15] = wt;
         }
         uint32_t f, k;

@@ -213,9 +213,6 @@ __global__ __launch_bounds__(kBlock) void sha1_ragged_kernel(const uint8_t* __re
 //   consumer: sync  for b { C(b) <- slot b&1; sync }
 // so P(b+1) overlaps C(b) on the other slot.
 // ---------------------------------------------------------------------------
-struct SplitLds {
-    uint4 w[2][20][64];
-};
 
 __device__ __forceinline__ void expand_store(uint32_t (&w)[16], uint4 (*dst)[64], int lane) {
 #pragma unroll
@@ -226,7 +223,7 @@ __device__ __forceinline__ void expand_store(uint32_t (&w)[16], uint4 (*dst)[64]
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int t = 4 * q + j;
-            const uint32_t x = rotl(VX_PAR(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]) ^ w[t & 15], 1);
+            const uint32_t x = rotl(VX_XOR2(VX_PAR(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15]), w[t & 15]), 1);
             w[t & 15] = x;
             v[j] = x;
         }
@@ -272,6 +269,166 @@ __device__ __forceinline__ void rounds_lds(State& s, const uint4 (*src)[64], int
     s.h4 += e;
 }
 
+// ---------------------------------------------------------------------------
+// Ring protocol between the producer and consumer waves, S slots of 80 words.
+//  S = 2: the producer is one block ahead; the consumer reads block b from
+//         LDS at the top of block b and stalls on those 20 ds_read_b128.
+//  S = 3: the producer is two blocks ahead, so the consumer reads block b+1
+//         into a second register set WHILE it compresses block b: no LDS
+//         wait on the chain (60 KiB per pair: 2 pairs per CU instead of 4).
+// Both waves pass 1 + nb_wave barriers:
+//   producer: for b { P(b) -> slot(b); publish(b) }  producer_done
+//   consumer: consume (initial barrier, then one per block)
+// ---------------------------------------------------------------------------
+template <int S>
+struct RingLds {
+    uint4 w[S][20][64];
+};
+
+template <int S>
+__device__ __forceinline__ uint32_t ring_slot(uint32_t b) {
+    return S == 2 ? (b & 1u) : (b % 3u);
+}
+
+// Producer: block b is in its slot.  S = 3 publishes blocks 0 and 1 together.
+template <int S>
+__device__ __forceinline__ void publish(uint32_t b) {
+    if (S == 2 || b >= 1) __syncthreads();
+}
+
+template <int S>
+__device__ __forceinline__ void producer_done(uint32_t nb_wave) {
+    if (S == 2) {
+        __syncthreads();
+    } else if (nb_wave) {
+        __syncthreads();
+        __syncthreads();
+    }
+}
+
+__device__ __forceinline__ void load_w(uint4 (&r)[20], const uint4 (*src)[64], int lane) {
+#pragma unroll
+    for (int q = 0; q < 20; ++q) r[q] = src[q][lane];
+}
+
+__device__ __forceinline__ void rounds_regs(State& s, const uint4 (&w)[20]) {
+    uint32_t a = s.h0, b = s.h1, c = s.h2, d = s.h3, e = s.h4;
+#pragma unroll
+    for (int q = 0; q < 20; ++q) {
+        const uint32_t wq[4] = {w[q].x, w[q].y, w[q].z, w[q].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int t = 4 * q + j;
+            uint32_t f, k;
+            if (t < 20) {
+                f = VX_CH(b, c, d);
+                k = kK0;
+            } else if (t < 40) {
+                f = VX_PAR(b, c, d);
+                k = kK1;
+            } else if (t < 60) {
+                f = VX_MAJ(b, c, d);
+                k = kK2;
+            } else {
+                f = VX_PAR(b, c, d);
+                k = kK3;
+            }
+            const uint32_t tmp = rotl(a, 5) + f + e + k + wq[j];
+            e = d;
+            d = c;
+            c = rotl(b, 30);
+            b = a;
+            a = tmp;
+        }
+    }
+    s.h0 += a;
+    s.h1 += b;
+    s.h2 += c;
+    s.h3 += d;
+    s.h4 += e;
+}
+
+// Consumer: compress blocks [0, nb_wave).  kSelect: blocks >= b1 commit only
+// for lanes with b < nb (ragged phase 2); otherwise b1 == nb_wave == nb.
+// Align the next loop's first instruction to 64 bytes (s_nop padding, run
+// once on the way in).  The consumer loop is an issue-bound chain of ~430
+// instructions per block, and its speed depended on where the code object put
+// it: the SAME 2-slot kernel ran config 3 in 57.3 ms when its loop head sat on a
+// 32-byte boundary and 67.4 ms when it sat at 4 mod 32 (a build that only
+// changed which other kernels were instantiated; profiles/r01/align/).
+#define VX_ALIGN_NEXT_LOOP()                    \
+    do {                                        \
+        __builtin_amdgcn_sched_barrier(0);      \
+        asm volatile(".p2align 6");             \
+        __builtin_amdgcn_sched_barrier(0);      \
+    } while (0)
+
+template <int S, bool kSelect>
+__device__ __forceinline__ void consume(State& s, RingLds<S>& lds, int lane, uint32_t nb_wave, uint32_t b1,
+                                        uint32_t nb) {
+    if (S == 2) {
+        __syncthreads();
+        VX_ALIGN_NEXT_LOOP();
+        for (uint32_t b = 0; b < b1; ++b) {
+            rounds_lds(s, lds.w[b & 1], lane);
+            __syncthreads();
+        }
+        if (kSelect) {
+            VX_ALIGN_NEXT_LOOP();
+            for (uint32_t b = b1; b < nb_wave; ++b) {
+                State t = s;
+                rounds_lds(t, lds.w[b & 1], lane);
+                if (b < nb) s = t;
+                __syncthreads();
+            }
+        }
+        return;
+    }
+    if (nb_wave == 0) return;
+    auto step = [&](uint32_t b, const uint4 (&r)[20]) {
+        if (!kSelect || b < b1) {
+            rounds_regs(s, r);
+        } else {
+            State t = s;
+            rounds_regs(t, r);
+            if (b < nb) s = t;
+        }
+        // The state must exist before the next barrier: without this hipcc
+        // sinks the whole block's rounds below the s_barrier (they only feed
+        // later blocks), and the barrier's lgkmcnt(0) then waits on the
+        // freshly issued reads with nothing to overlap them.
+        asm volatile("" : "+v"(s.h0), "+v"(s.h1), "+v"(s.h2), "+v"(s.h3), "+v"(s.h4));
+    };
+    // sched_barrier(0) keeps the scheduler from moving the next block's
+    // ds_reads into or past the rounds.
+    uint4 r0[20], r1[20];
+    __syncthreads();
+    load_w(r0, lds.w[0], lane);
+    // Drain block 0's reads before the loop: hipcc's waitcnt pass merges the
+    // loop entry with the back edge, and with these 20 reads still pending on
+    // entry it put an lgkmcnt(14) on the next block's fresh reads in EVERY
+    // trip (the 4-bit counter saturates).  lgkmcnt(0), other counters max.
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    uint32_t b = 0;
+    for (; b + 2 <= nb_wave; b += 2) {
+        load_w(r1, lds.w[ring_slot<S>(b + 1)], lane);
+        __builtin_amdgcn_sched_barrier(0);
+        step(b, r0);
+        __builtin_amdgcn_sched_barrier(0);
+        __syncthreads();
+        if (b + 2 < nb_wave) load_w(r0, lds.w[ring_slot<S>(b + 2)], lane);
+        __builtin_amdgcn_sched_barrier(0);
+        step(b + 1, r1);
+        __builtin_amdgcn_sched_barrier(0);
+        __syncthreads();
+    }
+    if (b < nb_wave) {
+        step(b, r0);
+        __builtin_amdgcn_sched_barrier(0);
+        __syncthreads();
+    }
+}
+
 __device__ __forceinline__ void le_words(uint32_t (&w)[16], const uint4& q0, const uint4& q1, const uint4& q2,
                                          const uint4& q3) {
     const uint4 q[4] = {q0, q1, q2, q3};
@@ -301,13 +458,14 @@ __device__ __forceinline__ void tail_words(uint32_t (&w)[16], const uint8_t* q, 
     }
 }
 
+template <int S>
 __global__ __launch_bounds__(kPairBlock) void sha1_split_kernel(const uint8_t* __restrict__ base, uint64_t stride,
                                                                 uint32_t len, uint32_t n,
                                                                 uint8_t* __restrict__ digests,
                                                                 const uint8_t* __restrict__ expected,
                                                                 uint8_t* __restrict__ matched,
                                                                 const uint32_t* __restrict__ exp_index) {
-    __shared__ SplitLds lds;
+    __shared__ RingLds<S> lds;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t i = blockIdx.x * 64 + lane;
@@ -340,12 +498,12 @@ __global__ __launch_bounds__(kPairBlock) void sha1_split_kernel(const uint8_t* _
                     load_group(ring[(r + R - 1) % R], src + (size_t)gl * 8);
                     if (g0 + r < ng) {
                         le_words(w, ring[r][0], ring[r][1], ring[r][2], ring[r][3]);
-                        expand_store(w, lds.w[b & 1], lane);
-                        __syncthreads();
+                        expand_store(w, lds.w[ring_slot<S>(b)], lane);
+                        publish<S>(b);
                         ++b;
                         le_words(w, ring[r][4], ring[r][5], ring[r][6], ring[r][7]);
-                        expand_store(w, lds.w[b & 1], lane);
-                        __syncthreads();
+                        expand_store(w, lds.w[ring_slot<S>(b)], lane);
+                        publish<S>(b);
                         ++b;
                     }
                 }
@@ -355,8 +513,8 @@ __global__ __launch_bounds__(kPairBlock) void sha1_split_kernel(const uint8_t* _
         if (nfull & 1) {
             const uint4* q4 = reinterpret_cast<const uint4*>(q);
             le_words(w, q4[0], q4[1], q4[2], q4[3]);
-            expand_store(w, lds.w[b & 1], lane);
-            __syncthreads();
+            expand_store(w, lds.w[ring_slot<S>(b)], lane);
+            publish<S>(b);
             ++b;
             q += 64;
         }
@@ -366,39 +524,42 @@ __global__ __launch_bounds__(kPairBlock) void sha1_split_kernel(const uint8_t* _
         if (rem <= 55) {
             w[14] = bits_hi;
             w[15] = bits_lo;
-            expand_store(w, lds.w[b & 1], lane);
-            __syncthreads();
+            expand_store(w, lds.w[ring_slot<S>(b)], lane);
+            publish<S>(b);
         } else {
-            expand_store(w, lds.w[b & 1], lane);
-            __syncthreads();
+            expand_store(w, lds.w[ring_slot<S>(b)], lane);
+            publish<S>(b);
             ++b;
 #pragma unroll
             for (int k = 0; k < 14; ++k) w[k] = 0;
             w[14] = bits_hi;
             w[15] = bits_lo;
-            expand_store(w, lds.w[b & 1], lane);
-            __syncthreads();
+            expand_store(w, lds.w[ring_slot<S>(b)], lane);
+            publish<S>(b);
         }
-        __syncthreads();
+        producer_done<S>(nb);
     } else {
         // ---------------- consumer ----------------
         State s = iv();
-        __syncthreads();
-        for (uint32_t b = 0; b < nb; ++b) {
-            rounds_lds(s, lds.w[b & 1], lane);
-            __syncthreads();
-        }
+        consume<S, false>(s, lds, lane, nb, nb, nb);
         if (i < n) emit(s, i, digests, expected, matched, exp_index);
     }
+}
+
+template <int S>
+hipError_t launch_uniform_split_s(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
+                                  const uint8_t* expected, uint8_t* matched, hipStream_t stream,
+                                  const uint32_t* exp_index) {
+    const uint32_t blocks = (n + 63) / 64;
+    hipLaunchKernelGGL(sha1_split_kernel<S>, dim3(blocks), dim3(kPairBlock), 0, stream, base, stride, len, n,
+                       digests, expected, matched, exp_index);
+    return hipGetLastError();
 }
 
 hipError_t launch_uniform_split(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
                                 const uint8_t* expected, uint8_t* matched, hipStream_t stream,
                                 const uint32_t* exp_index) {
-    const uint32_t blocks = (n + 63) / 64;
-    hipLaunchKernelGGL(sha1_split_kernel, dim3(blocks), dim3(kPairBlock), 0, stream, base, stride, len, n, digests,
-                       expected, matched, exp_index);
-    return hipGetLastError();
+    return launch_uniform_split_s<kSplitSlots>(base, stride, len, n, digests, expected, matched, stream, exp_index);
 }
 
 
@@ -446,14 +607,14 @@ __device__ __forceinline__ void pad_words(uint32_t (&w)[16], const uint8_t* q, u
 // poffs[j] == 0); a chunk that ends the piece pads with the piece's total
 // length and emits digest/verdict for row pid, any other chunk (a multiple of
 // 64 bytes) stores the state back.
-template <bool kChunked>
+template <bool kChunked, int S>
 __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
     const uint8_t* __restrict__ base, const uint64_t* __restrict__ offsets, const uint32_t* __restrict__ lens,
     const uint32_t* __restrict__ order, uint32_t n, uint8_t* __restrict__ digests,
     const uint8_t* __restrict__ expected, uint8_t* __restrict__ matched, const uint32_t* __restrict__ exp_index,
     const uint32_t* __restrict__ pids, const uint64_t* __restrict__ poffs, const uint64_t* __restrict__ tlens,
     uint32_t* __restrict__ states) {
-    __shared__ SplitLds lds;
+    __shared__ RingLds<S> lds;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t j = blockIdx.x * 64 + lane;
@@ -499,8 +660,8 @@ __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
                     load_block(ring[(r + R - 1) % R], src + (size_t)bl * 4);
                     __builtin_amdgcn_sched_barrier(0);
                     le_words(w, ring[r][0], ring[r][1], ring[r][2], ring[r][3]);
-                    expand_store(w, lds.w[(b0 + r) & 1], lane);
-                    __syncthreads();
+                    expand_store(w, lds.w[ring_slot<S>(b0 + r)], lane);
+                    publish<S>(b0 + r);
                 }
             }
         }
@@ -545,13 +706,13 @@ __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
                             if (k >= 14) v = (is_pad1 && rem > 55) ? (k == 14 ? bits_hi : bits_lo) : v;
                             w[k] = v;
                         }
-                        expand_store(w, lds.w[b & 1], lane);
-                        __syncthreads();
+                        expand_store(w, lds.w[ring_slot<S>(b)], lane);
+                        publish<S>(b);
                     }
                 }
             }
         }
-        __syncthreads();
+        producer_done<S>(nb_wave);
     } else {
         // ---------------- consumer ----------------
         State s = iv();
@@ -559,17 +720,7 @@ __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
             const uint32_t* st = states + (size_t)pid * 5;
             s = State{st[0], st[1], st[2], st[3], st[4]};
         }
-        __syncthreads();
-        for (uint32_t b = 0; b < b1; ++b) {
-            rounds_lds(s, lds.w[b & 1], lane);
-            __syncthreads();
-        }
-        for (uint32_t b = b1; b < nb_wave; ++b) {
-            State t = s;
-            rounds_lds(t, lds.w[b & 1], lane);
-            if (b < nb) s = t;
-            __syncthreads();
-        }
+        consume<S, true>(s, lds, lane, nb_wave, b1, nb);
         if (j < n) {
             if (!kChunked || final_chunk) {
                 emit(s, pid, digests, expected, matched, exp_index);
@@ -585,13 +736,22 @@ __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
     }
 }
 
+template <int S>
+hipError_t launch_ragged_split_s(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens,
+                                 const uint32_t* order, uint32_t n, uint8_t* digests, const uint8_t* expected,
+                                 uint8_t* matched, hipStream_t stream, const uint32_t* exp_index) {
+    const uint32_t blocks = (n + 63) / 64;
+    hipLaunchKernelGGL((sha1_ragged_split_kernel<false, S>), dim3(blocks), dim3(kPairBlock), 0, stream, base,
+                       offsets, lens, order, n, digests, expected, matched, exp_index, nullptr, nullptr, nullptr,
+                       nullptr);
+    return hipGetLastError();
+}
+
 hipError_t launch_ragged_split(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens,
                                const uint32_t* order, uint32_t n, uint8_t* digests, const uint8_t* expected,
                                uint8_t* matched, hipStream_t stream, const uint32_t* exp_index) {
-    const uint32_t blocks = (n + 63) / 64;
-    hipLaunchKernelGGL(sha1_ragged_split_kernel<false>, dim3(blocks), dim3(kPairBlock), 0, stream, base, offsets,
-                       lens, order, n, digests, expected, matched, exp_index, nullptr, nullptr, nullptr, nullptr);
-    return hipGetLastError();
+    return launch_ragged_split_s<kSplitSlots>(base, offsets, lens, order, n, digests, expected, matched, stream,
+                                              exp_index);
 }
 
 hipError_t launch_chunk(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens, uint32_t n,
@@ -599,7 +759,7 @@ hipError_t launch_chunk(const uint8_t* base, const uint64_t* offsets, const uint
                         uint8_t* digests, const uint8_t* expected, uint8_t* matched, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const uint32_t blocks = (n + 63) / 64;
-    hipLaunchKernelGGL(sha1_ragged_split_kernel<true>, dim3(blocks), dim3(kPairBlock), 0, stream, base, offsets,
+    hipLaunchKernelGGL((sha1_ragged_split_kernel<true, kSplitSlots>), dim3(blocks), dim3(kPairBlock), 0, stream, base, offsets,
                        lens, nullptr, n, digests, expected, matched, nullptr, pids, poffs, tlens, states);
     return hipGetLastError();
 }
@@ -640,6 +800,10 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, ui
                           const uint32_t* exp_index) {
     if (variant == kUniformLane) return launch_uniform_lane(base, stride, len, n, digests, expected, matched, stream, exp_index);
     if (variant == kUniformSplit) return launch_uniform_split(base, stride, len, n, digests, expected, matched, stream, exp_index);
+    if (variant == kSplitRing2)
+        return launch_uniform_split_s<2>(base, stride, len, n, digests, expected, matched, stream, exp_index);
+    if (variant == kSplitRing3)
+        return launch_uniform_split_s<3>(base, stride, len, n, digests, expected, matched, stream, exp_index);
     // Default: the integer VALU is the roofline once every SIMD has a wave
     // (n >= 65,536 with the lane kernel), and the split kernel's extra LDS
     // hand-off only costs there.  Below kSplitMaxPieces the chip has idle
@@ -676,6 +840,10 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
                          uint32_t n, uint8_t* digests, const uint8_t* expected, uint8_t* matched,
                          hipStream_t stream, int variant, const uint32_t* exp_index) {
     if (variant == kUniformLane) return launch_ragged_lane(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
+    if (variant == kSplitRing2)
+        return launch_ragged_split_s<2>(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
+    if (variant == kSplitRing3)
+        return launch_ragged_split_s<3>(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
     return launch_ragged_split(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
 }
 }  // namespace vx
