@@ -2,9 +2,10 @@
 // against the C ABI (include/vx_hash.h), without io_uring or sockets.
 //
 // What it mirrors (reference file:line):
-//  * BufferPool of piece_length page-aligned mmap buffers, MAP_POPULATE
-//    (torrent.rs:344, buf_pool.rs:92-133, buf_ring.rs:24-42) — registered
-//    with vx_register_host_buffer so completed pieces DMA straight to the GPU.
+//  * BufferPool of 256 piece_length buffers, each its OWN anonymous
+//    MAP_POPULATE mmap as in vortex (torrent.rs:344, buf_pool.rs:92-98,
+//    buf_ring.rs:24-42), each registered with vx_register_host_buffer so the
+//    batch's gather kernel pulls completed pieces straight to the GPU.
 //  * Piece::on_subpiece copies each 16 KiB subpiece into the piece buffer
 //    (piece_selector.rs:381-398); when the piece is complete it is handed to
 //    the hasher (peer_connection.rs:1122-1158) → vx_submit.
@@ -96,16 +97,18 @@ int main(int argc, char** argv) {
         std::fprintf(stderr, "vx_create: %d %s\n", rc, vx_last_error());
         return 1;
     }
-    // BufferPool: 256 buffers of piece_length (torrent.rs:344), one mmap.
+    // BufferPool: 256 buffers of piece_length (torrent.rs:344), one mmap each.
     const uint32_t nbuf = 256;
-    const size_t pool_bytes = (size_t)nbuf * plen;
-    uint8_t* pool = static_cast<uint8_t*>(
-        mmap(nullptr, pool_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_POPULATE, -1, 0));
-    if (pool == MAP_FAILED) return 1;
-    std::memset(pool, 0xEE, pool_bytes);  // stale bytes: never zeroed between uses
-    if (int rc = vx_register_host_buffer(ctx, pool, pool_bytes)) {
-        std::fprintf(stderr, "register: %d %s\n", rc, vx_last_error());
-        return 1;
+    std::vector<uint8_t*> pool(nbuf);
+    for (uint32_t b = 0; b < nbuf; ++b) {
+        void* m = mmap(nullptr, plen, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_POPULATE, -1, 0);
+        if (m == MAP_FAILED) return 1;
+        pool[b] = static_cast<uint8_t*>(m);
+        std::memset(pool[b], 0xEE, plen);  // stale bytes: never zeroed between uses
+        if (int rc = vx_register_host_buffer(ctx, pool[b], plen)) {
+            std::fprintf(stderr, "register: %d %s\n", rc, vx_last_error());
+            return 1;
+        }
     }
     std::vector<uint32_t> free_bufs;
     for (uint32_t b = 0; b < nbuf; ++b) free_bufs.push_back(nbuf - 1 - b);
@@ -142,13 +145,13 @@ int main(int argc, char** argv) {
             for (uint32_t k = 0; k < subs_per_turn && d.next_sub < d.nsub; ++k, ++d.next_sub) {
                 const uint32_t off = d.next_sub * kSubpiece;
                 const uint32_t sl = std::min(kSubpiece, d.len - off);
-                uint8_t* dst = pool + (size_t)d.buf * plen + off;
+                uint8_t* dst = pool[d.buf] + off;
                 gen_range(seed, d.piece, off, sl, dst);
                 if (d.corrupt && d.next_sub == d.nsub / 2) dst[sl / 3] ^= 0x40;
             }
             if (d.next_sub == d.nsub) {  // complete → hash (peer_connection.rs:1145)
                 const uint64_t tag = (tag_seq++ << 32) | d.piece;
-                const uint8_t* buf = pool + (size_t)d.buf * plen;
+                const uint8_t* buf = pool[d.buf];
                 if (int rc = vx_submit(ctx, tag, buf, d.len, &expected[(size_t)d.piece * 20])) {
                     std::fprintf(stderr, "vx_submit: %d %s\n", rc, vx_last_error());
                     return 1;
@@ -201,9 +204,9 @@ int main(int argc, char** argv) {
         }
     }
     const double el = now_ms() - t0;
-    vx_unregister_host_buffer(ctx, pool);
+    for (uint8_t* b : pool) vx_unregister_host_buffer(ctx, b);
     vx_destroy(ctx);
-    munmap(pool, pool_bytes);
+    for (uint8_t* b : pool) munmap(b, plen);
     std::sort(lat.begin(), lat.end());
     auto pct = [&](double q) { return lat.empty() ? 0.0 : lat[std::min(lat.size() - 1, (size_t)(q * lat.size()))]; };
     std::printf(

@@ -668,3 +668,52 @@ def test_lazy_flush_launches_from_poll(built, gpu):
             time.sleep(0.001)
     assert sorted(got) == list(range(12))
     assert all(got[i].hash_matched and got[i].digest == want[i] for i in got)
+
+
+@pytest.mark.parametrize("chunk", [None, 32 * 1024])
+def test_gather_batch_chunked(built, gpu, monkeypatch, chunk):
+    """A host batch whose pieces sit in separately registered buffers (vortex's
+    BufferPool: one mmap per buffer, buf_pool.rs:92-98), ragged lengths with
+    the longest >= 2 chunks, takes the chunked gather path:
+    each round's chunk bytes are pulled by the gather kernel.  Digests and
+    verdicts bit-exact vs hashlib/the oracle and vs the whole-piece path."""
+    import mmap
+
+    from vortex_amd import _lib
+    from vortex_amd.hash_pool import HashPool
+
+    if chunk is not None:
+        monkeypatch.setenv("VX_BATCH_CHUNK", str(chunk))
+    rng = random.Random(11)
+    lens = [(1 << 20) + 3, 262144, 0, 64, 200000, 131072 + 16, 5, (1 << 20), 700000] * 5
+    rng.shuffle(lens)
+    bufs = [mmap.mmap(-1, max(L, 1) + 4096) for L in lens]
+    gen = np.random.default_rng(12)
+    pieces = []
+    for b, L in zip(bufs, lens):
+        np.frombuffer(b, dtype=np.uint8)[:] = gen.integers(0, 256, len(b), dtype=np.uint8)  # stale tail bytes too
+        pieces.append(memoryview(b)[:L])
+    want = [hashlib.sha1(p).digest() for p in pieces]
+    assert want[1] == oracle.sha1(bytes(pieces[1]))
+    exp = [w if i % 7 else bytes(20) for i, w in enumerate(want)]
+    with HashPool(max(lens), slots=3, slot_bytes=4 << 20) as pool:  # 4 MiB slots: several windows
+        for b in bufs:
+            pool.register_buffer(b)
+        r0 = _lib.lib().vx_tuning_chunk_rounds(pool._h)
+        t0 = _lib.lib().vx_tuning_gather_tiles(pool._h)
+        dig = pool.sha1_batch(pieces)
+        matched, dig2 = pool.verify_batch(pieces, exp)
+        rounds = _lib.lib().vx_tuning_chunk_rounds(pool._h) - r0
+        tiles = _lib.lib().vx_tuning_gather_tiles(pool._h) - t0
+        for b in bufs:
+            pool.unregister_buffer(b)
+    assert dig == want and dig2 == want
+    assert matched == [i % 7 != 0 for i in range(len(lens))]
+    C = chunk or 65536
+    assert rounds > 0
+    assert tiles == 2 * sum((L + C - 1) // C for L in lens)  # one tile per chunk (C <= 64 KiB)
+    monkeypatch.setenv("VX_BATCH_CHUNK", "0")
+    with HashPool(max(lens), slots=3, slot_bytes=4 << 20) as pool:
+        matched0, dig0 = pool.verify_batch(pieces, exp)  # unregistered: whole-piece staged path
+        assert _lib.lib().vx_tuning_chunk_rounds(pool._h) == 0
+    assert matched0 == matched and dig0 == want

@@ -7,7 +7,7 @@ OUT=gpurun_out/async/sweep_${1:-run}.jsonl
 : > $OUT
 for pl in 16384 262144 2097152 4194304; do
   for fe in 64 512; do
-    for reg in 1 0; do
+    for reg in 2 1 0; do
       gib=4; [ $pl -eq 16384 ] && gib=1
       timeout -k 10 120 ./tools/native/async_probe $pl 1024 $gib $fe $reg >> $OUT || { echo "FAIL pl=$pl fe=$fe reg=$reg"; exit 1; }
     done

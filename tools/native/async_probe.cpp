@@ -11,6 +11,9 @@
 // line: GiB/s of piece bytes submitted → verdict polled.
 //
 // usage: async_probe <piece_len> [nbuf=1024] [total_GiB=8] [flush_every=64] [registered=1] [slot_MiB=default]
+//   registered: 0 = plain memory (staged), 1 = one registered mmap holding all
+//   buffers, 2 = one mmap per buffer, each registered (vortex's BufferPool,
+//   buf_pool.rs:92-98)
 #include <sys/mman.h>
 
 #include <algorithm>
@@ -38,7 +41,7 @@ int main(int argc, char** argv) {
     const uint32_t nbuf = argc > 2 ? (uint32_t)std::atoi(argv[2]) : 1024;
     const double total_gib = argc > 3 ? std::atof(argv[3]) : 8.0;
     const uint32_t flush_every = argc > 4 ? (uint32_t)std::atoi(argv[4]) : 64;
-    const bool registered = argc > 5 ? std::atoi(argv[5]) != 0 : true;
+    const int registered = argc > 5 ? std::atoi(argv[5]) : 1;
     const uint64_t total = (uint64_t)(total_gib * (1ull << 30) / plen);
 
     vx_config cfg;
@@ -53,20 +56,37 @@ int main(int argc, char** argv) {
         return 1;
     }
     const size_t pool_bytes = (size_t)nbuf * plen;
-    uint8_t* pool = static_cast<uint8_t*>(
-        mmap(nullptr, pool_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_POPULATE, -1, 0));
-    if (pool == MAP_FAILED) return 1;
-    std::mt19937_64 rng(plen);
-    for (size_t i = 0; i < pool_bytes / 8; ++i) reinterpret_cast<uint64_t*>(pool)[i] = rng();
-    if (registered) {
-        if (int rc = vx_register_host_buffer(ctx, pool, pool_bytes)) {
-            std::fprintf(stderr, "register: %d %s\n", rc, vx_last_error());
-            return 1;
-        }
-    }
+    std::vector<uint8_t*> maps;  // what to unregister / unmap
+    auto map = [&](size_t bytes) -> uint8_t* {
+        void* m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_POPULATE, -1, 0);
+        return m == MAP_FAILED ? nullptr : static_cast<uint8_t*>(m);
+    };
     std::vector<const uint8_t*> ptrs(nbuf);
     std::vector<uint32_t> lens(nbuf, plen);
-    for (uint32_t b = 0; b < nbuf; ++b) ptrs[b] = pool + (size_t)b * plen;
+    if (registered == 2) {
+        for (uint32_t b = 0; b < nbuf; ++b) {
+            uint8_t* m = map(plen);
+            if (!m) return 1;
+            maps.push_back(m);
+            ptrs[b] = m;
+        }
+    } else {
+        uint8_t* pool = map(pool_bytes);
+        if (!pool) return 1;
+        maps.push_back(pool);
+        for (uint32_t b = 0; b < nbuf; ++b) ptrs[b] = pool + (size_t)b * plen;
+    }
+    std::mt19937_64 rng(plen);
+    for (uint32_t b = 0; b < nbuf; ++b)
+        for (size_t i = 0; i < plen / 8; ++i) reinterpret_cast<uint64_t*>(const_cast<uint8_t*>(ptrs[b]))[i] = rng();
+    const size_t map_bytes = registered == 2 ? plen : pool_bytes;
+    if (registered) {
+        for (uint8_t* m : maps)
+            if (int rc = vx_register_host_buffer(ctx, m, map_bytes)) {
+                std::fprintf(stderr, "register: %d %s\n", rc, vx_last_error());
+                return 1;
+            }
+    }
     std::vector<uint8_t> digests((size_t)nbuf * 20);
     if (int rc = vx_sha1_batch(ctx, ptrs.data(), lens.data(), nbuf, digests.data())) {
         std::fprintf(stderr, "vx_sha1_batch: %d %s\n", rc, vx_last_error());
@@ -115,12 +135,13 @@ int main(int argc, char** argv) {
     }
     if (vx_drain(ctx, 0) || poll()) return 1;
     const double el = now_s() - t0;
-    if (registered) vx_unregister_host_buffer(ctx, pool);
+    if (registered)
+        for (uint8_t* m : maps) vx_unregister_host_buffer(ctx, m);
     vx_destroy(ctx);
-    munmap(pool, pool_bytes);
+    for (uint8_t* m : maps) munmap(m, map_bytes);
     std::printf("{\"piece_len\": %u, \"pieces\": %llu, \"registered\": %d, \"flush_every\": %u, \"GiBps\": %.3f, "
                 "\"mismatched\": %llu, \"polled\": %llu}\n",
-                plen, (unsigned long long)total, registered ? 1 : 0, flush_every,
+                plen, (unsigned long long)total, registered, flush_every,
                 (double)total * plen / el / (1 << 30), (unsigned long long)bad, (unsigned long long)polled);
     return bad == 0 && polled == total ? 0 : 3;
 }
