@@ -107,7 +107,7 @@ int main() {
         for (size_t i = 0; i < n; ++i) off[i] = slot[i] * L;
         CK(hipMemcpy(d_off, off.data(), n * 8, hipMemcpyHostToDevice));
         const std::string tag = std::to_string(L >> 10) + "K";
-        for (int grid : {256, 1024, 4096}) {
+        for (int grid : {32, 64, 256, 1024}) {
             for (uint64_t tile : {uint64_t(16) << 10}) {
                 double best = 0;
                 for (int rep = 0; rep < 3; ++rep) {
@@ -119,6 +119,24 @@ int main() {
                 }
                 emit("kernel_" + tag + "_g" + std::to_string(grid), best);
             }
+        }
+        // one hipMemcpyBatchAsync of the same scattered pieces (SDMA, no CUs)
+        {
+            std::vector<void*> dsts(n), srcs(n);
+            std::vector<size_t> sizes(n, L);
+            for (size_t i = 0; i < n; ++i) {
+                dsts[i] = d + i * L;
+                srcs[i] = mm + off[i];
+            }
+            double best = 0;
+            for (int rep = 0; rep < 3; ++rep) {
+                size_t fail_idx = 0;
+                const double t0 = now();
+                CK(hipMemcpyBatchAsync(dsts.data(), srcs.data(), sizes.data(), n, nullptr, nullptr, 0, &fail_idx, st));
+                CK(hipStreamSynchronize(st));
+                best = std::max(best, bytes / (now() - t0) / (1 << 30));
+            }
+            emit("batchdma_" + tag, best);
         }
         // per-piece DMA of the same scattered pieces (bounded call count)
         if (n <= 8192) {

@@ -350,31 +350,16 @@ __device__ __forceinline__ void rounds_regs(State& s, const uint4 (&w)[20]) {
 
 // Consumer: compress blocks [0, nb_wave).  kSelect: blocks >= b1 commit only
 // for lanes with b < nb (ragged phase 2); otherwise b1 == nb_wave == nb.
-// Align the next loop's first instruction to 64 bytes (s_nop padding, run
-// once on the way in).  The consumer loop is an issue-bound chain of ~430
-// instructions per block, and its speed depended on where the code object put
-// it: the SAME 2-slot kernel ran config 3 in 57.3 ms when its loop head sat on a
-// 32-byte boundary and 67.4 ms when it sat at 4 mod 32 (a build that only
-// changed which other kernels were instantiated; profiles/r01/align/).
-#define VX_ALIGN_NEXT_LOOP()                    \
-    do {                                        \
-        __builtin_amdgcn_sched_barrier(0);      \
-        asm volatile(".p2align 6");             \
-        __builtin_amdgcn_sched_barrier(0);      \
-    } while (0)
-
 template <int S, bool kSelect>
 __device__ __forceinline__ void consume(State& s, RingLds<S>& lds, int lane, uint32_t nb_wave, uint32_t b1,
                                         uint32_t nb) {
     if (S == 2) {
         __syncthreads();
-        VX_ALIGN_NEXT_LOOP();
         for (uint32_t b = 0; b < b1; ++b) {
             rounds_lds(s, lds.w[b & 1], lane);
             __syncthreads();
         }
         if (kSelect) {
-            VX_ALIGN_NEXT_LOOP();
             for (uint32_t b = b1; b < nb_wave; ++b) {
                 State t = s;
                 rounds_lds(t, lds.w[b & 1], lane);

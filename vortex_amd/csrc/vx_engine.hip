@@ -161,6 +161,7 @@ struct vx_ctx {
     // separately registered buffers: 29.7 -> 35.7 GiB/s.
     std::unordered_map<uintptr_t, Reg> registered_at;
     bool gather = true;        // VX_GATHER=0 turns the gather kernel off (A/B)
+    uint32_t gather_grid = 0;  // VX_GATHER_GRID: workgroups per gather launch (0 = default)
     uint64_t gather_tiles = 0;  // tiles gathered (vx_tuning_gather_tiles)
     uint64_t pending = 0;
     uint64_t seq = 0;
@@ -384,7 +385,8 @@ int launch_slot_impl(vx_ctx* c, int si) {
     if (s.gtiles) {
         VX_HIP(hipMemcpyAsync(s.d_src, s.h_src, (size_t)n * 8, hipMemcpyHostToDevice, cs));
         VX_HIP(hipMemcpyAsync(s.d_tfirst, s.h_tfirst, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, cs));
-        hipError_t e = vx::launch_gather(s.d_src, s.d_offsets, s.d_lens, s.d_tfirst, n, s.gtiles, s.d_arena, cs);
+        hipError_t e =
+            vx::launch_gather(s.d_src, s.d_offsets, s.d_lens, s.d_tfirst, n, s.gtiles, s.d_arena, cs, c->gather_grid);
         if (e != hipSuccess) return hip_fail(e, "gather launch");
         c->gather_tiles += s.gtiles;
     }
@@ -613,6 +615,7 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     c->cfg = *cfg;
     if (const char* m = std::getenv("VX_H2D_MODE")) c->h2d_mode = std::atoi(m) & 3;
     if (const char* m = std::getenv("VX_GATHER")) c->gather = std::atoi(m) != 0;
+    if (const char* m = std::getenv("VX_GATHER_GRID")) c->gather_grid = (uint32_t)std::atoi(m);
     if (const char* m = std::getenv("VX_LAZY_FLUSH")) c->lazy_flush = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_BATCH_CHUNK")) c->batch_chunk = align_up(std::strtoull(m, nullptr, 0), kAlign);
     int rc = set_device(c);
@@ -1185,7 +1188,7 @@ int batch_chunked_gather(vx_ctx* c, const uint32_t* lens, const uint8_t* expecte
                         hipSuccess)
                     return fail(VX_EDEVICE, "batch: gather table H2D failed");
                 hipError_t e = vx::launch_gather(sl.d_src, sl.d_offsets, sl.d_lens, sl.d_tfirst, m, tiles,
-                                                 sl.d_arena, st);
+                                                 sl.d_arena, st, c->gather_grid);
                 if (e != hipSuccess) return hip_fail(e, "batch: gather launch");
                 c->gather_tiles += tiles;
                 return 0;

@@ -23,7 +23,7 @@ namespace vx {
 
 constexpr uint32_t kGatherTile = 64 * 1024;
 constexpr int kGatherBlock = 256;
-constexpr int kGatherGrid = 256;  // one workgroup per CU saturates PCIe (probe: g256 53.5, g1024 52.0 GiB/s)
+constexpr int kGatherGrid = 64;  // workgroups per launch (see the note above launch_gather)
 
 __global__ __launch_bounds__(kGatherBlock) void gather_kernel(const uint64_t* __restrict__ src,
                                                               const uint64_t* __restrict__ dst_off,
@@ -68,10 +68,19 @@ __global__ __launch_bounds__(kGatherBlock) void gather_kernel(const uint64_t* __
 
 uint32_t gather_tiles(uint32_t len) { return (len + kGatherTile - 1) / kGatherTile; }
 
+// Grid size.  64 workgroups already move 52.8 GiB/s alone (256: 52.8, 32:
+// 52.3; profiles/r01/h2d/gather3.json), and a gather runs BESIDE hash kernels
+// (the next chunk round, other slots).  With 256 workgroups the slow host
+// reads in flight starved a concurrent chunk kernel's HBM loads: the kernel
+// took 1.74 ms instead of 0.83 (rocprofv3 trace, profiles/r01/async/), and
+// one-mmap-per-piece 2 MiB batches ran at 35 GiB/s.  At 64: 49.4 GiB/s; async
+// 256 KiB pieces 42 -> 47 GiB/s.
+
 hipError_t launch_gather(const uint64_t* src, const uint64_t* dst_off, const uint32_t* lens, const uint32_t* tfirst,
-                         uint32_t n, uint32_t ntiles, uint8_t* arena, hipStream_t stream) {
+                         uint32_t n, uint32_t ntiles, uint8_t* arena, hipStream_t stream, uint32_t max_grid) {
     if (n == 0 || ntiles == 0) return hipSuccess;
-    const uint32_t grid = ntiles < (uint32_t)kGatherGrid ? ntiles : (uint32_t)kGatherGrid;
+    const uint32_t cap = max_grid ? max_grid : (uint32_t)kGatherGrid;
+    const uint32_t grid = ntiles < cap ? ntiles : cap;
     hipLaunchKernelGGL(gather_kernel, dim3(grid), dim3(kGatherBlock), 0, stream, src, dst_off, lens, tfirst, n,
                        arena);
     return hipGetLastError();

@@ -61,7 +61,7 @@ hipError_t launch_chunk(const uint8_t* base, const uint64_t* offsets, const uint
 // [tfirst[i], tfirst[i+1]) of the ntiles = tfirst[n] total.
 uint32_t gather_tiles(uint32_t len);
 hipError_t launch_gather(const uint64_t* src, const uint64_t* dst_off, const uint32_t* lens, const uint32_t* tfirst,
-                         uint32_t n, uint32_t ntiles, uint8_t* arena, hipStream_t stream);
+                         uint32_t n, uint32_t ntiles, uint8_t* arena, hipStream_t stream, uint32_t max_grid = 0);
 
 hipError_t launch_synth_fill(uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint64_t first,
                              uint64_t seed, uint32_t corrupt_every, hipStream_t stream);
