@@ -15,11 +15,11 @@ constexpr int kPairBlock = 128;  // split kernel: consumer wave + producer wave
 // 1 = lane-per-piece (one wave does everything), 2 = producer/consumer split.
 enum UniformVariant { kUniformDefault = 0, kUniformLane = 1, kUniformSplit = 2, kSplitRing2 = 3, kSplitRing3 = 4 };
 // LDS ring slots of the split kernels (sha1_kernels.hip "Ring protocol").
-// 2: the consumer reads each block at its top.  3 (variant 4, kept for A/B):
-// the producer runs two blocks ahead and the consumer prefetches the next
-// block into registers while compressing; measured 6-14 % SLOWER on every
-// chain-bound batch, so the default stays 2.
-constexpr int kSplitSlots = 2;
+// 3: the producer runs two blocks ahead and the consumer prefetches the next
+// block into registers while compressing (config 5 geometry 28.1 -> 26.6 ms,
+// DESIGN.md §3.2).  2: the consumer reads each block at its top.  Variants
+// 3 / 4 pin 2 / 3 slots for A/B runs.
+constexpr int kSplitSlots = 3;
 constexpr uint32_t kSplitMaxPieces = 16384;  // default picks split at or below this batch size
 
 hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
