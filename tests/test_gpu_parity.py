@@ -489,6 +489,42 @@ def test_verify_files_chunked(built, gpu, tmp_path, pl, slot_mib, batch):
     assert not all(got) and any(got)
 
 
+@pytest.mark.parametrize("chunk,ramp,pl", [(65536, 1, 2 << 20), (262144, 1, (1 << 20) + 3072),
+                                           (131072, 0, (1 << 20) + 3072), (4096, 1, 300000)])
+def test_verify_files_chunk_schedule(built, gpu, tmp_path, monkeypatch, chunk, ramp, pl):
+    """Re-verify round schedules: other chunk sizes, and the
+    head/tail ramp (C/4, C/4, C/2 ... C/2, C/4, rest) with piece lengths that
+    are not multiples of C/4.  Small slots force several windows, so the ramp
+    applies only to the first and last; a range call starts mid-torrent."""
+    from vortex_amd.hash_pool import HashPool
+
+    monkeypatch.setenv("VX_VERIFY_CHUNK", str(chunk))
+    monkeypatch.setenv("VX_VERIFY_RAMP", str(ramp))
+    sizes = [3 * pl + 777, 0, 5 * pl + 64, pl // 3]
+    paths = []
+    for k, L in enumerate(sizes):
+        p = tmp_path / f"s{k}.bin"
+        p.write_bytes(oracle.gen_piece(13, k, L))
+        paths.append(str(p))
+    data = b"".join(open(p, "rb").read() for p in paths)
+    exp = b"".join(hashlib.sha1(data[i:i + pl]).digest() for i in range(0, len(data), pl))
+    n = len(exp) // 20
+    slot = max(4 << 20, 3 * chunk)  # a few pieces' chunks per window
+    with HashPool(pl, slots=3, batch_pieces=4, slot_bytes=max(slot, pl)) as pool:
+        got, bad = pool.verify_files(paths, sizes, pl, exp, io_threads=3)
+        assert got == [True] * n and bad == 0
+        with open(paths[2], "r+b") as f:  # flip a byte in the last C/4 of a piece
+            f.seek(2 * pl - 100)
+            b = f.read(1)
+            f.seek(2 * pl - 100)
+            f.write(bytes([b[0] ^ 1]))
+        got, bad = pool.verify_files(paths, sizes, pl, exp, io_threads=3)
+        sub, sub_bad = pool.verify_files(paths, sizes, pl, exp, io_threads=2, first=3, count=n - 4)
+    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=3)
+    assert got == want and not all(got)
+    assert sub == want[3:n - 1]
+
+
 def test_api_misuse_and_lifecycle(built, gpu):
     """Errors are codes, never aborts: busy-state checks, bad rows, and
     destroy with work in flight (drains like the reference's scope join)."""

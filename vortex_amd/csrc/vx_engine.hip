@@ -133,6 +133,11 @@ struct vx_ctx {
     int h2d_mode = 2;
     // Chunk bytes for strided host batches of long pieces (§6.4); 0 = off.
     uint64_t batch_chunk = 64 * 1024;
+    // Chunk bytes of the file re-verify (§6.3), and whether its first and
+    // last rounds ramp down to C/4 (VX_VERIFY_CHUNK / VX_VERIFY_RAMP; the
+    // ramp takes config 5 from 45.5 to 47.7 GiB/s, profiles/r01/reverify/).
+    uint64_t verify_chunk = 256 * 1024;
+    bool verify_ramp = true;
     uint64_t chunk_rounds = 0;  // chunk rounds launched (vx_tuning_chunk_rounds)
     // Per-piece device rows of the chunk paths (state | expected | digest |
     // verdict), kept across calls and grown on demand: allocating them per
@@ -618,6 +623,9 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (const char* m = std::getenv("VX_GATHER_GRID")) c->gather_grid = (uint32_t)std::atoi(m);
     if (const char* m = std::getenv("VX_LAZY_FLUSH")) c->lazy_flush = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_BATCH_CHUNK")) c->batch_chunk = align_up(std::strtoull(m, nullptr, 0), kAlign);
+    if (const char* m = std::getenv("VX_VERIFY_CHUNK"))
+        c->verify_chunk = std::max<uint64_t>(4096, align_up(std::strtoull(m, nullptr, 0), 4096));
+    if (const char* m = std::getenv("VX_VERIFY_RAMP")) c->verify_ramp = std::atoi(m) != 0;
     int rc = set_device(c);
     if (!rc && c->h2d_mode == 3 && hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess)
         rc = fail(VX_EDEVICE, "vx_create: copy stream");
@@ -989,10 +997,37 @@ struct ChunkPipe {
     }
 };
 
+// Round boundaries [a, a + len) over a window whose longest piece is L:
+// chunks of C, and with `head`/`tail` the first / last C bytes split C/4,
+// C/4, C/2 (resp. C/2, C/4, C/4), so the first read and the last chain —
+// the parts of the pipeline nothing overlaps — are a quarter as long.  Every
+// boundary is a multiple of C/4 (>= 1 KiB, so of the 64-byte block).
+std::vector<std::pair<uint64_t, uint64_t>> chunk_schedule(uint64_t L, uint64_t C, bool head, bool tail) {
+    std::vector<std::pair<uint64_t, uint64_t>> r;
+    const uint64_t q = C / 4;
+    uint64_t a = 0;
+    if (L == 0) r.push_back({0, 0});
+    if (head && L > 2 * C)
+        for (uint64_t len : {q, q, 2 * q}) r.push_back({a, len}), a += len;
+    // the tail ramp covers the last R bytes, R in (C - q, C]: 2q, q, R - 3q
+    const uint64_t tail_from = tail && L > 2 * C ? (L - C + q - 1) / q * q : L;
+    while (a < tail_from) {
+        const uint64_t len = std::min(C, tail_from - a);
+        r.push_back({a, len});
+        a += len;
+    }
+    if (a < L) {
+        r.push_back({a, 2 * q});
+        r.push_back({a + 2 * q, q});
+        r.push_back({a + 3 * q, L - a - 3 * q});
+    }
+    return r;
+}
+
 int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl, uint64_t total, uint64_t first,
                    uint64_t end) {
     vx_ctx* c = fv.c;
-    const uint64_t C = kChunkBytes;
+    const uint64_t C = c->verify_chunk;
     const uint64_t last_len = total - (n - 1) * (uint64_t)pl;
     const uint64_t cnt = end - first;
     ChunkPipe cp(c);
@@ -1001,10 +1036,13 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     // windows of W pieces; each window runs its rounds in order
     const Slot& s0 = c->slots[0];
     const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>(s0.cap, s0.arena_cap / C));
-    const uint64_t rounds = (pl + C - 1) / C;
     for (uint64_t w0 = first; w0 < end && !rc; w0 += W) {
         const uint64_t w1 = std::min<uint64_t>(end, w0 + W);
-        for (uint64_t k = 0; k < rounds && !rc; ++k) {
+        const uint64_t wmax = w1 == n ? std::max<uint64_t>(pl, last_len) : pl;
+        const auto sched = chunk_schedule(wmax, C, c->verify_ramp && w0 == first, c->verify_ramp && w1 == end);
+        for (size_t k = 0; k < sched.size() && !rc; ++k) {
+            const uint64_t a = sched[k].first, rlen = sched[k].second;
+            const uint64_t pitch = align_up(rlen, kAlign);
             const int si = cp.free_slot([&] { fv.consume(); });
             if (si < 0) {
                 rc = si;
@@ -1017,11 +1055,10 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
             uint32_t m = 0;
             for (uint64_t i = w0; i < w1; ++i) {
                 const uint64_t len_i = i == n - 1 ? last_len : pl;
-                const uint64_t a = k * C;
                 if (a >= len_i && !(a == 0 && len_i == 0)) continue;  // piece already finished
-                const uint64_t clen = std::min<uint64_t>(C, len_i - a);
-                items.push_back(vx_files::ReadItem{s.h_stage + (uint64_t)m * C, i, a, clen});
-                s.h_offsets[m] = (uint64_t)m * C;
+                const uint64_t clen = std::min<uint64_t>(rlen, len_i - a);
+                items.push_back(vx_files::ReadItem{s.h_stage + (uint64_t)m * pitch, i, a, clen});
+                s.h_offsets[m] = (uint64_t)m * pitch;
                 s.h_lens[m] = (uint32_t)clen;
                 s.h_pidx[m] = (uint32_t)(i - first);
                 s.h_poff[m] = a;
@@ -1030,7 +1067,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
             }
             if (m == 0) continue;
             rd.run(items);
-            s.bytes = (uint64_t)(m - 1) * C + s.h_lens[m - 1];
+            s.bytes = (uint64_t)(m - 1) * pitch + s.h_lens[m - 1];
             rc = cp.round(si, m, k > 0, [&](Slot& sl, hipStream_t st) {
                 if (hipMemcpyAsync(sl.d_arena, sl.h_stage, sl.bytes, hipMemcpyHostToDevice, st) != hipSuccess)
                     return fail(VX_EDEVICE, "vx_verify_files: chunk H2D failed");
@@ -1277,7 +1314,7 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
         return fail(VX_EINVAL, "vx_verify_files: n_pieces does not match the files' total length");
     if (count == 0) return 0;
     const bool chunked = piece_length > kChunkBytes;
-    if (chunked ? c->slots[0].arena_cap < kChunkBytes : piece_length > c->cfg.max_piece_len)
+    if (chunked ? c->slots[0].arena_cap < c->verify_chunk : piece_length > c->cfg.max_piece_len)
         return fail(VX_ERANGE, "vx_verify_files: pieces do not fit the context's slots");
     int rc = set_device(c);
     if (rc) return rc;
