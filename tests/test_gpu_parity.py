@@ -490,7 +490,8 @@ def test_verify_files_chunked(built, gpu, tmp_path, pl, slot_mib, batch):
 
 
 @pytest.mark.parametrize("chunk,ramp,pl", [(65536, 1, 2 << 20), (262144, 1, (1 << 20) + 3072),
-                                           (131072, 0, (1 << 20) + 3072), (4096, 1, 300000)])
+                                           (131072, 0, (1 << 20) + 3072), (4096, 1, 300000),
+                                           (None, 1, 300000), (None, 1, 2 << 20), (None, 1, 262144)])
 def test_verify_files_chunk_schedule(built, gpu, tmp_path, monkeypatch, chunk, ramp, pl):
     """Re-verify round schedules: other chunk sizes, and the
     head/tail ramp (C/4, C/4, C/2 ... C/2, C/4, rest) with piece lengths that
@@ -498,7 +499,8 @@ def test_verify_files_chunk_schedule(built, gpu, tmp_path, monkeypatch, chunk, r
     applies only to the first and last; a range call starts mid-torrent."""
     from vortex_amd.hash_pool import HashPool
 
-    monkeypatch.setenv("VX_VERIFY_CHUNK", str(chunk))
+    if chunk is not None:  # None: the per-call policy (verify_chunk_for)
+        monkeypatch.setenv("VX_VERIFY_CHUNK", str(chunk))
     monkeypatch.setenv("VX_VERIFY_RAMP", str(ramp))
     sizes = [3 * pl + 777, 0, 5 * pl + 64, pl // 3]
     paths = []
@@ -509,7 +511,7 @@ def test_verify_files_chunk_schedule(built, gpu, tmp_path, monkeypatch, chunk, r
     data = b"".join(open(p, "rb").read() for p in paths)
     exp = b"".join(hashlib.sha1(data[i:i + pl]).digest() for i in range(0, len(data), pl))
     n = len(exp) // 20
-    slot = max(4 << 20, 3 * chunk)  # a few pieces' chunks per window
+    slot = max(4 << 20, 3 * (chunk or 262144))  # a few pieces' chunks per window
     with HashPool(pl, slots=3, batch_pieces=4, slot_bytes=max(slot, pl)) as pool:
         got, bad = pool.verify_files(paths, sizes, pl, exp, io_threads=3)
         assert got == [True] * n and bad == 0

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--dir", default=os.environ.get("TMPDIR", "/tmp"))
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--piece-len", type=int, default=2097152,
+                    help="piece length over the same file size (<= 256 KiB takes the whole-piece path)")
     ap.add_argument("--cpu-between", action="store_true",
                     help="run the CPU pool restatement before every GPU run (as reverify_bench does)")
     a = ap.parse_args()
@@ -36,8 +38,8 @@ def main():
     import oracle
     from vortex_amd.hash_pool import HashPool
 
-    pl = 2097152
-    total = 2907832320 if a.scale >= 1.0 else int(2907832320 * a.scale) // pl * pl + 1179648
+    pl = a.piece_len
+    total = 2907832320 if a.scale >= 1.0 else int(2907832320 * a.scale) // 2097152 * 2097152 + 1179648
     n = (total + pl - 1) // pl
     last = total - (n - 1) * pl
     path = os.path.join(a.dir, "vx_reverify_sweep.iso")
@@ -56,7 +58,7 @@ def main():
     for env in envs:
         saved = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
-        pools.append(HashPool(pl, slots=4, slot_bytes=512 << 20, batch_pieces=4096))
+        pools.append(HashPool(pl, slots=4, slot_bytes=512 << 20, batch_pieces=max(4096, (512 << 20) // pl)))
         for k, v in saved.items():
             if v is None:
                 os.environ.pop(k, None)
@@ -82,7 +84,7 @@ def main():
         for p in pools:
             p.close()
         os.unlink(path)
-    out = {"workload": f"re-verify {n} x 2 MiB pieces ({total} B) from a warm file, {a.threads} io threads",
+    out = {"workload": f"re-verify {n} x {pl} B pieces ({total} B) from a warm file, {a.threads} io threads",
            "GiBps": res, "median": {c: sorted(v)[len(v) // 2] for c, v in res.items()}}
     print(json.dumps(out))
 

@@ -133,11 +133,14 @@ struct vx_ctx {
     int h2d_mode = 2;
     // Chunk bytes for strided host batches of long pieces (§6.4); 0 = off.
     uint64_t batch_chunk = 64 * 1024;
-    // Chunk bytes of the file re-verify (§6.3), and whether its first and
-    // last rounds ramp down to C/4 (VX_VERIFY_CHUNK / VX_VERIFY_RAMP; the
-    // ramp takes config 5 from 45.5 to 47.7 GiB/s, profiles/r01/reverify/).
-    uint64_t verify_chunk = 256 * 1024;
+    // Chunk bytes of the file re-verify (§6.3; 0 = chosen per call by
+    // verify_chunk_for), whether its first and last rounds ramp down to C/4,
+    // and the piece length above which it chunks (0 = pieces >= 2 chunks).
+    // Env overrides: VX_VERIFY_CHUNK, VX_VERIFY_RAMP, VX_VERIFY_CHUNKED_ABOVE.
+    uint64_t verify_chunk = 0;
     bool verify_ramp = true;
+    uint64_t verify_chunked_above = 0;
+    bool verify_overlap = true;  // read round k+1 while round k is enqueued (VX_VERIFY_OVERLAP)
     uint64_t chunk_rounds = 0;  // chunk rounds launched (vx_tuning_chunk_rounds)
     // Per-piece device rows of the chunk paths (state | expected | digest |
     // verdict), kept across calls and grown on demand: allocating them per
@@ -626,6 +629,8 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (const char* m = std::getenv("VX_VERIFY_CHUNK"))
         c->verify_chunk = std::max<uint64_t>(4096, align_up(std::strtoull(m, nullptr, 0), 4096));
     if (const char* m = std::getenv("VX_VERIFY_RAMP")) c->verify_ramp = std::atoi(m) != 0;
+    if (const char* m = std::getenv("VX_VERIFY_CHUNKED_ABOVE")) c->verify_chunked_above = std::strtoull(m, nullptr, 0);
+    if (const char* m = std::getenv("VX_VERIFY_OVERLAP")) c->verify_overlap = std::atoi(m) != 0;
     int rc = set_device(c);
     if (!rc && c->h2d_mode == 3 && hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess)
         rc = fail(VX_EDEVICE, "vx_create: copy stream");
@@ -792,7 +797,7 @@ uint64_t vx_pending(const vx_ctx* c) { return c ? c->pending : 0; }
 
 // Bulk re-verify from disk (include/vx_hash.h).
 //
-// Pieces up to kChunkBytes: the reader threads pread each slot's pieces
+// Pieces shorter than two chunks (verify_chunk_for): the reader threads pread each slot's pieces
 // straight into that slot's pinned stage (segments back to back,
 // file_store.rs:240-298 byte ranges) and the slot launches while the next free
 // slot is read.  Longer pieces: resumable chunked hashing — round k reads
@@ -803,7 +808,6 @@ uint64_t vx_pending(const vx_ctx* c) { return c ? c->pending : 0; }
 }  // extern "C" (the helpers below are C++ templates)
 
 namespace {
-constexpr uint64_t kChunkBytes = 256 * 1024;
 
 struct FileVerify {
     vx_ctx* c;
@@ -831,46 +835,80 @@ struct FileVerify {
     }
 };
 
+// Re-verify chunk size for `count` pieces: 256 KiB when
+// every piece's chunk fits one slot arena (a single window of rounds), else
+// 128 KiB.  A call split into windows ends on its last, smaller window, whose
+// rounds are chain-bound; measured (profiles/r01/reverify/policy*.json):
+// 1 MiB x 2,774 pieces 43.6 -> 46.8 GiB/s at 128 KiB, 256 KiB x 11,093 pieces
+// 37.5 (whole-piece slots) -> 45.0, 2 MiB x 1,387 best at 256 KiB + ramp.
+uint64_t verify_chunk_for(const vx_ctx* c, uint64_t count) {
+    if (c->verify_chunk) return c->verify_chunk;
+    constexpr uint64_t big = 256 * 1024, small = 128 * 1024;
+    return count * big <= c->slots[0].arena_cap && count <= c->slots[0].cap ? big : small;
+}
+
 // Both verify pieces [first, end) of an n-piece torrent; tags, bad[] and
-// matched_out are indexed from `first`.
+// matched_out are indexed from `first`.  Both read slot k+1 while slot k is
+// launched (see verify_chunked).
 int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl, uint64_t total, uint64_t first,
                  uint64_t end) {
     vx_ctx* c = fv.c;
     const uint64_t stride = align_up(pl, kAlign);
     const uint64_t last_len = total - (n - 1) * (uint64_t)pl;
-    std::vector<vx_files::ReadItem> items;
+    std::vector<vx_files::ReadItem> items[2];
+    int buf = 0, prev = -1;
+    auto launch_prev = [&]() -> int {
+        if (prev < 0) return 0;
+        int r = launch_slot(c, prev);
+        prev = -1;
+        if (!r) r = reap(c, false);
+        fv.consume();
+        return r;
+    };
     uint64_t next = first;
     int rc = 0;
     while (next < end && !rc) {
+        if ((c->slots.size() < 2 || !c->verify_overlap) && (rc = launch_prev())) break;  // one slot: nothing to overlap with
         const int si = fv.free_slot();
-        if (si < 0) return si;
+        if (si < 0) {
+            rc = si;
+            break;
+        }
         Slot& s = c->slots[si];
         reset_fill(s);
-        if ((rc = ensure_stage(s))) return rc;
+        if ((rc = ensure_stage(s))) break;
+        s.state = Slot::FILLING;  // reserved while the previous slot may still be unlaunched
         const uint64_t cap = std::min<uint64_t>(s.cap, std::max<uint64_t>(1, s.arena_cap / stride));
         const uint64_t lo = next, hi = std::min<uint64_t>(end, next + cap);
-        items.clear();
+        auto& it = items[buf];
+        buf ^= 1;
+        it.clear();
         for (uint64_t i = lo; i < hi; ++i) {
             const uint32_t len = (uint32_t)(i == n - 1 ? last_len : pl);
             const uint32_t k = (uint32_t)(i - lo);
-            items.push_back(vx_files::ReadItem{s.h_stage + k * stride, i, 0, len});
+            it.push_back(vx_files::ReadItem{s.h_stage + k * stride, i, 0, len});
             s.h_offsets[k] = k * stride;
             s.h_lens[k] = len;
             if (len != s.h_lens[0]) s.uniform = false;
             std::memcpy(s.h_expected + (size_t)k * 20, fv.expected + 20 * i, 20);
             s.tags.push_back(i - first);
         }
-        rd.run(items);
         s.n = (uint32_t)(hi - lo);
         s.has_expected = true;
         s.bytes = (hi - lo - 1) * stride + s.h_lens[s.n - 1];
         s.runs.push_back(Run{0, s.bytes});
-        s.state = Slot::FILLING;
-        rc = launch_slot(c, si);
+        rd.start(it);
+        rc = launch_prev();  // the previous slot, while this one reads
+        rd.wait();
+        prev = si;
         next = hi;
-        if (!rc) rc = reap(c, false);
-        fv.consume();
     }
+    if (!rc) rc = launch_prev();
+    for (auto& sl : c->slots)  // a slot read but never launched (error path)
+        if (sl.state == Slot::FILLING) {
+            reset_fill(sl);
+            sl.state = Slot::FREE;
+        }
     return rc;
 }
 
@@ -1024,18 +1062,50 @@ std::vector<std::pair<uint64_t, uint64_t>> chunk_schedule(uint64_t L, uint64_t C
     return r;
 }
 
+// Round k+1 is read while round k is enqueued: the enqueue (chain_h2d waits
+// for the copy two rounds back, then metadata copies and the launch) took
+// 0.8-0.9 ms of host time per 256 KiB round, and with the read (5.5 ms) in
+// series the host needed 6.4 ms per round against a 6.35 ms H2D, so the copy
+// engine idled between rounds (VX_TRACE_ROUNDS).
 int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl, uint64_t total, uint64_t first,
-                   uint64_t end) {
+                   uint64_t end, uint64_t C) {
     vx_ctx* c = fv.c;
-    const uint64_t C = c->verify_chunk;
     const uint64_t last_len = total - (n - 1) * (uint64_t)pl;
     const uint64_t cnt = end - first;
     ChunkPipe cp(c);
     int rc = cp.open(cnt, fv.expected + 20 * first, "vx_verify_files");
-    std::vector<vx_files::ReadItem> items;
+    std::vector<vx_files::ReadItem> items[2];  // round k+1 reads while round k's are still referenced
     // windows of W pieces; each window runs its rounds in order
     const Slot& s0 = c->slots[0];
     const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>(s0.cap, s0.arena_cap / C));
+    // VX_TRACE_ROUNDS=1: per-round host timings on stderr
+    static const bool trace = [] {
+        const char* e = std::getenv("VX_TRACE_ROUNDS");
+        return e && e[0] == '1';
+    }();
+    using clk = std::chrono::steady_clock;
+    const auto t_call = clk::now();
+    auto ms = [](clk::time_point a, clk::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    struct Pending {
+        int si = -1;
+        uint32_t m = 0;
+        bool continues = false;
+    } prev;
+    auto enqueue = [&]() -> int {
+        if (prev.si < 0) return 0;
+        const auto t0 = clk::now();
+        const int r = cp.round(prev.si, prev.m, prev.continues, [&](Slot& sl, hipStream_t st) {
+            if (hipMemcpyAsync(sl.d_arena, sl.h_stage, sl.bytes, hipMemcpyHostToDevice, st) != hipSuccess)
+                return fail(VX_EDEVICE, "vx_verify_files: chunk H2D failed");
+            return 0;
+        });
+        if (trace) std::fprintf(stderr, "vx   enqueue slot %d: %.2f ms\n", prev.si, ms(t0, clk::now()));
+        prev.si = -1;
+        return r;
+    };
+    int buf = 0;
     for (uint64_t w0 = first; w0 < end && !rc; w0 += W) {
         const uint64_t w1 = std::min<uint64_t>(end, w0 + W);
         const uint64_t wmax = w1 == n ? std::max<uint64_t>(pl, last_len) : pl;
@@ -1043,7 +1113,10 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
         for (size_t k = 0; k < sched.size() && !rc; ++k) {
             const uint64_t a = sched[k].first, rlen = sched[k].second;
             const uint64_t pitch = align_up(rlen, kAlign);
+            if ((c->slots.size() < 2 || !c->verify_overlap) && (rc = enqueue())) break;  // one slot: nothing to overlap with
+            const auto t_a = clk::now();
             const int si = cp.free_slot([&] { fv.consume(); });
+            const auto t_b = clk::now();
             if (si < 0) {
                 rc = si;
                 break;
@@ -1051,13 +1124,16 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
             Slot& s = c->slots[si];
             reset_fill(s);
             if ((rc = ensure_stage(s))) break;
-            items.clear();
+            s.state = Slot::FILLING;  // reserved: the previous round may still be unlaunched
+            auto& it = items[buf];
+            buf ^= 1;
+            it.clear();
             uint32_t m = 0;
             for (uint64_t i = w0; i < w1; ++i) {
                 const uint64_t len_i = i == n - 1 ? last_len : pl;
                 if (a >= len_i && !(a == 0 && len_i == 0)) continue;  // piece already finished
                 const uint64_t clen = std::min<uint64_t>(rlen, len_i - a);
-                items.push_back(vx_files::ReadItem{s.h_stage + (uint64_t)m * pitch, i, a, clen});
+                it.push_back(vx_files::ReadItem{s.h_stage + (uint64_t)m * pitch, i, a, clen});
                 s.h_offsets[m] = (uint64_t)m * pitch;
                 s.h_lens[m] = (uint32_t)clen;
                 s.h_pidx[m] = (uint32_t)(i - first);
@@ -1065,17 +1141,29 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
                 s.h_tlen[m] = len_i;
                 ++m;
             }
-            if (m == 0) continue;
-            rd.run(items);
+            if (m == 0) {
+                s.state = Slot::FREE;
+                continue;
+            }
             s.bytes = (uint64_t)(m - 1) * pitch + s.h_lens[m - 1];
-            rc = cp.round(si, m, k > 0, [&](Slot& sl, hipStream_t st) {
-                if (hipMemcpyAsync(sl.d_arena, sl.h_stage, sl.bytes, hipMemcpyHostToDevice, st) != hipSuccess)
-                    return fail(VX_EDEVICE, "vx_verify_files: chunk H2D failed");
-                return 0;
-            });
+            const auto t_c = clk::now();
+            rd.start(it);
+            rc = enqueue();  // the previous round, while this one reads
+            rd.wait();
+            const auto t_d = clk::now();
+            prev = Pending{si, m, k > 0};
+            if (trace)
+                std::fprintf(stderr, "vx round %zu slot %d at %.2f: wait %.2f prep %.2f read+enqueue %.2f (%.1f GiB/s)\n",
+                             (size_t)k, si, ms(t_call, t_a), ms(t_a, t_b), ms(t_b, t_c), ms(t_c, t_d),
+                             s.bytes / (ms(t_c, t_d) * 1e-3) / (1 << 30));
         }
-        cp.end_window();
     }
+    if (!rc) rc = enqueue();
+    for (auto& sl : c->slots)  // a round read but never launched (error path)
+        if (sl.state == Slot::FILLING) {
+            reset_fill(sl);
+            sl.state = Slot::FREE;
+        }
     rc = cp.finish(fv.matched_out, nullptr, rc);
     if (!rc)
         for (uint64_t i = 0; i < cnt; ++i)
@@ -1313,8 +1401,10 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
     if (n_pieces != (total + piece_length - 1) / piece_length)
         return fail(VX_EINVAL, "vx_verify_files: n_pieces does not match the files' total length");
     if (count == 0) return 0;
-    const bool chunked = piece_length > kChunkBytes;
-    if (chunked ? c->slots[0].arena_cap < c->verify_chunk : piece_length > c->cfg.max_piece_len)
+    const uint64_t C = verify_chunk_for(c, count);
+    bool chunked = c->verify_chunked_above ? piece_length > c->verify_chunked_above : piece_length >= 2 * C;
+    if (piece_length > c->cfg.max_piece_len) chunked = true;  // whole pieces would not fit a slot
+    if (chunked ? c->slots[0].arena_cap < C : piece_length > c->cfg.max_piece_len)
         return fail(VX_ERANGE, "vx_verify_files: pieces do not fit the context's slots");
     int rc = set_device(c);
     if (rc) return rc;
@@ -1330,7 +1420,7 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
     {
         vx_files::Readers rd(nthreads, fs, fds, piece_length, bad.data(), first);
         FileVerify fv{c, expected, matched_out, bad};
-        rc = chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total, first, end)
+        rc = chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total, first, end, C)
                      : verify_whole(fv, rd, n_pieces, piece_length, total, first, end);
         if (!rc && !chunked) {
             while (fv.done < count && !rc) {

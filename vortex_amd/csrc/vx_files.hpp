@@ -136,6 +136,13 @@ class Readers {
     // lock-free counter let a worker that woke late for a finished
     // generation index the vector while the caller was refilling it.)
     void run(const std::vector<ReadItem>& items) {
+        start(items);
+        wait();
+    }
+    // start() hands `items` to the workers and returns; the caller must keep
+    // the vector unchanged until wait() returns, and wait() before the next
+    // start().  (The re-verify enqueues round k while round k+1 reads.)
+    void start(const std::vector<ReadItem>& items) {
         if (items.empty()) return;
         {
             std::lock_guard<std::mutex> g(mu_);
@@ -146,6 +153,8 @@ class Readers {
             ++gen_;
         }
         cv_.notify_all();
+    }
+    void wait() {
         std::unique_lock<std::mutex> g(mu_);
         done_cv_.wait(g, [&] { return left_ == 0; });
     }
