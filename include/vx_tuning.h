@@ -9,6 +9,7 @@
  */
 #ifndef VX_TUNING_H
 #define VX_TUNING_H
+#include <stddef.h>
 #include <stdint.h>
 #ifdef __cplusplus
 extern "C" {
@@ -18,7 +19,7 @@ int vx_sha1_device_ragged_variant(const void* d_base, const uint64_t* d_offsets,
                                   const uint32_t* d_order, uint32_t n, void* d_digests, const void* d_expected,
                                   void* d_matched, void* stream, int variant);
 /* Chunk rounds a context has launched on the resumable chunk paths (file
- * re-verify of pieces > 256 KiB, strided host batches).
+ * re-verify of pieces >= 2 chunks, strided host batches).
  * Tests use it to tell which path a batch took. */
 struct vx_ctx;
 uint64_t vx_tuning_chunk_rounds(const struct vx_ctx* ctx);
@@ -29,6 +30,11 @@ uint64_t vx_tuning_gather_tiles(const struct vx_ctx* ctx);
  * longest is max_len bytes, total_len bytes in all: 1 = lane, 2 = split
  * (host-only). */
 int vx_tuning_plan_ragged(uint32_t n, uint32_t max_len, uint64_t total_len);
+/* The file re-verify's round boundaries for a window whose longest piece is
+ * L bytes with chunk C (head/tail: ramp the first / last C bytes down to
+ * C/4).  Writes up to max (offset, length) pairs to out
+ * (2*max uint64_t) and returns the number of rounds (host-only). */
+size_t vx_tuning_chunk_schedule(uint64_t L, uint64_t C, int head, int tail, uint64_t* out, size_t max);
 
 int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
                                    const void* d_expected, void* d_matched, void* stream, int variant);

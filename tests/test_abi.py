@@ -123,3 +123,52 @@ def test_ragged_plan_host(built):
     assert plan(1387, 2 * MiB, 2907832320) == SPLIT                                # config 5 geometry
     assert plan(16384, 256 * KiB, 16384 * 256 * KiB) == SPLIT                      # chip not full
     assert plan(1 << 20, 16 * KiB, (1 << 20) * 16 * KiB) == LANE                   # many short pieces
+
+
+def _schedule(L, C, head, tail):
+    import ctypes
+
+    from vortex_amd import _lib
+
+    fn = _lib.lib().vx_tuning_chunk_schedule
+    n = fn(L, C, head, tail, None, 0)
+    out = (ctypes.c_uint64 * (2 * max(n, 1)))()
+    assert fn(L, C, head, tail, out, n) == n
+    return [(out[2 * i], out[2 * i + 1]) for i in range(n)]
+
+
+def test_chunk_schedule_known(built):
+    """Re-verify round boundaries at the config 5 geometry:
+    2 MiB with C = 256 KiB ramps 64K, 64K, 128K, 6 x 256K, 128K, 64K, 64K."""
+    KiB = 1024
+    got = _schedule(2048 * KiB, 256 * KiB, 1, 1)
+    assert [l // KiB for _, l in got] == [64, 64, 128] + [256] * 6 + [128, 64, 64]
+    assert _schedule(2048 * KiB, 256 * KiB, 0, 0) == [(k * 256 * KiB, 256 * KiB) for k in range(8)]
+    assert _schedule(256 * KiB, 128 * KiB, 1, 1) == [(0, 128 * KiB), (128 * KiB, 128 * KiB)]  # L = 2C: no ramp
+    assert _schedule(0, 256 * KiB, 1, 1) == [(0, 0)]  # an empty piece still gets its one padding round
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_chunk_schedule_properties(built, seed):
+    """Any L, C (multiple of 4 KiB), head/tail: rounds tile [0, L) in order,
+    no round exceeds C, every boundary but L is a multiple of C/4 (so of the
+    64-byte SHA-1 block: a non-final chunk never ends mid-block), the ramp's
+    first/last rounds are C/4 when L > 2C."""
+    import random
+
+    rng = random.Random(seed)
+    for _ in range(300):
+        C = rng.choice([4096, 65536, 131072, 262144, 393216, 524288])
+        L = rng.choice([rng.randrange(0, 4 * C), rng.randrange(0, 64 * C), 2 * C, 2 * C + 1, C - 1, C])
+        head, tail = rng.randrange(2), rng.randrange(2)
+        r = _schedule(L, C, head, tail)
+        a = 0
+        for off, ln in r:
+            assert off == a and 0 < ln <= C or (L == 0 and (off, ln) == (0, 0))
+            a += ln
+            if a < L:
+                assert a % (C // 4) == 0 and a % 64 == 0
+        assert a == L
+        if L > 2 * C:
+            assert (r[0][1] == C // 4) == bool(head)
+            assert (r[-1][1] <= C // 4) == bool(tail) or (not tail and L % C and L % C <= C // 4)

@@ -1512,6 +1512,16 @@ int vx_sha1_device_ragged_hint(const void* d_base, const uint64_t* d_offsets, co
 
 uint64_t vx_tuning_chunk_rounds(const vx_ctx* c) { return c ? c->chunk_rounds : 0; }
 uint64_t vx_tuning_gather_tiles(const vx_ctx* c) { return c ? c->gather_tiles : 0; }
+size_t vx_tuning_chunk_schedule(uint64_t L, uint64_t C, int head, int tail, uint64_t* out, size_t max) {
+    if (C < 4 || C % 4) return 0;
+    const auto r = chunk_schedule(L, C, head != 0, tail != 0);
+    for (size_t i = 0; i < r.size() && i < max && out; ++i) {
+        out[2 * i] = r[i].first;
+        out[2 * i + 1] = r[i].second;
+    }
+    return r.size();
+}
+
 int vx_tuning_plan_ragged(uint32_t n, uint32_t max_len, uint64_t total_len) {
     return vx::plan_ragged(n, max_len, total_len);
 }
