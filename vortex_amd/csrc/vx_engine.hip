@@ -600,13 +600,16 @@ void vx_config_default(vx_config* cfg, uint32_t max_piece_len) {
     cfg->max_piece_len = max_piece_len;
     cfg->slots = 4;
     // Throughput of the async path is bytes in flight / batch latency, and a
-    // batch's latency is its longest piece's chain (~28 ms at 2 MiB), so slots
-    // grow with the piece length: 128 pieces each, 128 MiB to 2 GiB of HBM.
-    // (The pinned stage is only allocated for unregistered pieces; keeping it
-    // at 128 MiB for short pieces keeps their staging memcpy cache-friendly:
-    // 256 MiB slots halved the unregistered 16 KiB rate, async_probe.)
+    // batch's latency is its longest piece's chain (~28 ms at 2 MiB: one lane
+    // hashes ~74 MB/s), so slots grow with the piece length: 512 pieces each,
+    // 128 MiB to 2 GiB of HBM.  128 pieces per slot held only ~512 lanes in
+    // flight over 4 slots; 512 took async 2 MiB pieces 25.7 -> 32.8 GiB/s and
+    // 4 MiB 22.3 -> 27.1 (profiles/r01/async/slot_sweep.jsonl).  (The pinned
+    // stage is only allocated for unregistered pieces; keeping it at 128 MiB
+    // for short pieces keeps their staging memcpy cache-friendly: 256 MiB
+    // slots halved the unregistered 16 KiB rate, async_probe.)
     const uint64_t piece = align_up(std::max<uint32_t>(max_piece_len, 1), kAlign);
-    cfg->slot_bytes = std::max(piece, std::min<uint64_t>(2ull << 30, std::max<uint64_t>(128ull << 20, piece * 128)));
+    cfg->slot_bytes = std::max(piece, std::min<uint64_t>(2ull << 30, std::max<uint64_t>(128ull << 20, piece * 512)));
     cfg->batch_pieces = (uint32_t)std::min<uint64_t>(65536, cfg->slot_bytes / align_up(std::max<uint32_t>(max_piece_len, 1), kAlign));
 }
 
