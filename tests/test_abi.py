@@ -150,25 +150,30 @@ def test_chunk_schedule_known(built):
 
 @pytest.mark.parametrize("seed", range(3))
 def test_chunk_schedule_properties(built, seed):
-    """Any L, C (multiple of 4 KiB), head/tail: rounds tile [0, L) in order,
-    no round exceeds C, every boundary but L is a multiple of C/4 (so of the
-    64-byte SHA-1 block: a non-final chunk never ends mid-block), the ramp's
-    first/last rounds are C/4 when L > 2C."""
+    """Any L, C (multiple of 4 KiB), head/tail ramp depths 0-3: rounds tile
+    [0, L) in order, no round exceeds C, every boundary but L is a multiple
+    of q = C / 2^(d+1) and of 64 (a non-final chunk never ends mid-block);
+    with L > 2C the ramped first round is q and the ramped last round <= q."""
     import random
 
     rng = random.Random(seed)
-    for _ in range(300):
+    for _ in range(400):
         C = rng.choice([4096, 65536, 131072, 262144, 393216, 524288])
         L = rng.choice([rng.randrange(0, 4 * C), rng.randrange(0, 64 * C), 2 * C, 2 * C + 1, C - 1, C])
-        head, tail = rng.randrange(2), rng.randrange(2)
+        head, tail = rng.randrange(4), rng.randrange(4)
+        d = max(head, tail)
+        q = C >> (d + 1)
         r = _schedule(L, C, head, tail)
         a = 0
         for off, ln in r:
             assert off == a and 0 < ln <= C or (L == 0 and (off, ln) == (0, 0))
             a += ln
             if a < L:
-                assert a % (C // 4) == 0 and a % 64 == 0
+                assert a % 64 == 0 and (d == 0 or q < 64 or a % q == 0)
         assert a == L
-        if L > 2 * C:
-            assert (r[0][1] == C // 4) == bool(head)
-            assert (r[-1][1] <= C // 4) == bool(tail) or (not tail and L % C and L % C <= C // 4)
+        if L > 2 * C and d and q >= 64:
+            assert (r[0][1] == q) == bool(head)
+            if tail:
+                assert r[-1][1] <= q and r[-2][1] == q
+        if L > 2 * C and (d == 0 or q < 64):
+            assert all(ln == C for _, ln in r[:-1])

@@ -138,7 +138,7 @@ struct vx_ctx {
     // and the piece length above which it chunks (0 = pieces >= 2 chunks).
     // Env overrides: VX_VERIFY_CHUNK, VX_VERIFY_RAMP, VX_VERIFY_CHUNKED_ABOVE.
     uint64_t verify_chunk = 0;
-    bool verify_ramp = true;
+    int verify_ramp = 1;  // ramp depth d: first/last rounds C / 2^(d+1) (0 = off)
     uint64_t verify_chunked_above = 0;
     bool verify_overlap = true;  // read round k+1 while round k is enqueued (VX_VERIFY_OVERLAP)
     uint64_t chunk_rounds = 0;  // chunk rounds launched (vx_tuning_chunk_rounds)
@@ -631,7 +631,7 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (const char* m = std::getenv("VX_BATCH_CHUNK")) c->batch_chunk = align_up(std::strtoull(m, nullptr, 0), kAlign);
     if (const char* m = std::getenv("VX_VERIFY_CHUNK"))
         c->verify_chunk = std::max<uint64_t>(4096, align_up(std::strtoull(m, nullptr, 0), 4096));
-    if (const char* m = std::getenv("VX_VERIFY_RAMP")) c->verify_ramp = std::atoi(m) != 0;
+    if (const char* m = std::getenv("VX_VERIFY_RAMP")) c->verify_ramp = std::max(0, std::min(5, std::atoi(m)));
     if (const char* m = std::getenv("VX_VERIFY_CHUNKED_ABOVE")) c->verify_chunked_above = std::strtoull(m, nullptr, 0);
     if (const char* m = std::getenv("VX_VERIFY_OVERLAP")) c->verify_overlap = std::atoi(m) != 0;
     int rc = set_device(c);
@@ -1039,28 +1039,35 @@ struct ChunkPipe {
 };
 
 // Round boundaries [a, a + len) over a window whose longest piece is L:
-// chunks of C, and with `head`/`tail` the first / last C bytes split C/4,
-// C/4, C/2 (resp. C/2, C/4, C/4), so the first read and the last chain —
-// the parts of the pipeline nothing overlaps — are a quarter as long.  Every
-// boundary is a multiple of C/4 (>= 1 KiB, so of the 64-byte block).
-std::vector<std::pair<uint64_t, uint64_t>> chunk_schedule(uint64_t L, uint64_t C, bool head, bool tail) {
+// chunks of C, and with `head`/`tail` ramps of depth d (q = C / 2^(d+1)) on
+// the first / last C bytes: q, q, 2q, ..., C/2 up front and C/2, ..., 2q, q,
+// rest (<= q) at the end, so the first read and the last chain — the parts
+// of the pipeline nothing overlaps — shrink to q.  d = 1 is C/4, C/4, C/2.
+// Every boundary is a multiple of q (>= 64 bytes for C >= 4 KiB, d <= 5), so
+// no non-final chunk ends mid-block.
+std::vector<std::pair<uint64_t, uint64_t>> chunk_schedule(uint64_t L, uint64_t C, int head, int tail) {
     std::vector<std::pair<uint64_t, uint64_t>> r;
-    const uint64_t q = C / 4;
+    const int d = std::max(head, tail);
+    const uint64_t q = C >> (d + 1);
     uint64_t a = 0;
     if (L == 0) r.push_back({0, 0});
-    if (head && L > 2 * C)
-        for (uint64_t len : {q, q, 2 * q}) r.push_back({a, len}), a += len;
-    // the tail ramp covers the last R bytes, R in (C - q, C]: 2q, q, R - 3q
-    const uint64_t tail_from = tail && L > 2 * C ? (L - C + q - 1) / q * q : L;
+    const bool ramp = d > 0 && q >= 64 && L > 2 * C;
+    if (ramp && head) {
+        r.push_back({a, q});
+        a += q;
+        for (uint64_t len = q; len < C; len *= 2) r.push_back({a, len}), a += len;
+    }
+    // the tail ramp covers the last R bytes, R in (C - q, C]: C/2, ..., q, R - (C - q)
+    const uint64_t tail_from = ramp && tail ? (L - C + q - 1) / q * q : L;
     while (a < tail_from) {
         const uint64_t len = std::min(C, tail_from - a);
         r.push_back({a, len});
         a += len;
     }
     if (a < L) {
-        r.push_back({a, 2 * q});
-        r.push_back({a + 2 * q, q});
-        r.push_back({a + 3 * q, L - a - 3 * q});
+        for (uint64_t len = C / 2; len >= q; len /= 2) r.push_back({a, len}), a += len;
+        r.push_back({a, L - a});
+        a = L;
     }
     return r;
 }
@@ -1112,7 +1119,8 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     for (uint64_t w0 = first; w0 < end && !rc; w0 += W) {
         const uint64_t w1 = std::min<uint64_t>(end, w0 + W);
         const uint64_t wmax = w1 == n ? std::max<uint64_t>(pl, last_len) : pl;
-        const auto sched = chunk_schedule(wmax, C, c->verify_ramp && w0 == first, c->verify_ramp && w1 == end);
+        const auto sched =
+            chunk_schedule(wmax, C, w0 == first ? c->verify_ramp : 0, w1 == end ? c->verify_ramp : 0);
         for (size_t k = 0; k < sched.size() && !rc; ++k) {
             const uint64_t a = sched[k].first, rlen = sched[k].second;
             const uint64_t pitch = align_up(rlen, kAlign);
@@ -1517,7 +1525,7 @@ uint64_t vx_tuning_chunk_rounds(const vx_ctx* c) { return c ? c->chunk_rounds : 
 uint64_t vx_tuning_gather_tiles(const vx_ctx* c) { return c ? c->gather_tiles : 0; }
 size_t vx_tuning_chunk_schedule(uint64_t L, uint64_t C, int head, int tail, uint64_t* out, size_t max) {
     if (C < 4 || C % 4) return 0;
-    const auto r = chunk_schedule(L, C, head != 0, tail != 0);
+    const auto r = chunk_schedule(L, C, std::max(0, std::min(5, head)), std::max(0, std::min(5, tail)));
     for (size_t i = 0; i < r.size() && i < max && out; ++i) {
         out[2 * i] = r[i].first;
         out[2 * i + 1] = r[i].second;
