@@ -491,7 +491,8 @@ def test_verify_files_chunked(built, gpu, tmp_path, pl, slot_mib, batch):
 
 @pytest.mark.parametrize("chunk,ramp,pl", [(65536, 1, 2 << 20), (262144, 1, (1 << 20) + 3072),
                                            (131072, 0, (1 << 20) + 3072), (4096, 1, 300000),
-                                           (None, 1, 300000), (None, 1, 2 << 20), (None, 1, 262144)])
+                                           (None, 1, 300000), (None, 1, 2 << 20), (None, 1, 262144),
+                                           (65536, 3, (1 << 20) + 3072)])
 def test_verify_files_chunk_schedule(built, gpu, tmp_path, monkeypatch, chunk, ramp, pl):
     """Re-verify round schedules: other chunk sizes, and the
     head/tail ramp (C/4, C/4, C/2 ... C/2, C/4, rest) with piece lengths that
