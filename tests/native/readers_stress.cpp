@@ -1,7 +1,9 @@
 // readers_stress.cpp — CPU test of vx_files::Readers (the pread pool behind
 // vx_verify_files): many back-to-back run() generations whose item vector the
-// caller rebuilds (and regrows) between runs, as verify_whole / verify_chunked
-// do.  Every item must land the right file bytes.  Built plain and with
+// caller rebuilds (and regrows) between runs; then the pipelined form
+// verify_whole / verify_chunked use (start(g), check generation g-1's bytes
+// while g reads into the other stage, wait(g); two item vectors alternating).
+// Every item must land the right file bytes.  Built plain and with
 // -fsanitize=thread by tests/test_native_cpu.py; exit 0 = ok.
 //
 // usage: readers_stress <scratch_file> [generations=3000] [threads=6]
@@ -53,6 +55,30 @@ int main(int argc, char** argv) {
                 if (std::memcmp(it.dst, file.data() + (size_t)it.piece * pl + it.start, it.len) != 0) ++errors;
             }
         }
+        // pipelined: generation g reads into stage2[g & 1] from items2[g & 1]
+        // while the caller checks generation g-1 (the other stage); a worker
+        // still touching g-1's vector or stage after wait() would show here
+        std::vector<vx_files::ReadItem> items2[2];
+        std::vector<uint8_t> stage2[2] = {std::vector<uint8_t>((size_t)pl * 64), std::vector<uint8_t>((size_t)pl * 64)};
+        auto check = [&](const std::vector<vx_files::ReadItem>& its) {
+            for (const auto& it : its)
+                if (std::memcmp(it.dst, file.data() + (size_t)it.piece * pl + it.start, it.len) != 0) ++errors;
+        };
+        for (int g = 0; g < gens; ++g) {
+            auto& its = items2[g & 1];
+            its.clear();
+            its.shrink_to_fit();
+            const uint32_t m = 1 + rng() % 64;
+            const uint32_t base = rng() % (npieces - m);
+            for (uint32_t k = 0; k < m; ++k) {
+                const uint32_t a = rng() % 2 ? 0 : 2048;
+                its.push_back(vx_files::ReadItem{stage2[g & 1].data() + (size_t)k * pl, base + k, a, pl - a});
+            }
+            rd.start(its);
+            if (g > 0) check(items2[(g - 1) & 1]);  // the previous generation, during this one's reads
+            rd.wait();
+        }
+        if (gens > 0) check(items2[(gens - 1) & 1]);
     }
     close(fds[0]);
     for (uint8_t b : bad) errors += b;
