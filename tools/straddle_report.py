@@ -21,7 +21,9 @@ LLVM = "/opt/rocm/lib/llvm/bin"
 def disassemble(obj: str) -> str:
     with tempfile.TemporaryDirectory() as d:
         fb, co = os.path.join(d, "fb.bin"), os.path.join(d, "dev.co")
-        subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", obj], check=True)
+        # an explicit output file: with only an input, objcopy rewrites it in place
+        subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fb}", obj, os.path.join(d, "scratch.o")],
+                       check=True)
         subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o", f"--input={fb}",
                         "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
         return subprocess.run([f"{LLVM}/llvm-objdump", "-d", co], check=True, capture_output=True,
