@@ -30,6 +30,9 @@
  *  - Threading (mirrors the reference): one thread (the io_uring event-loop
  *    thread) submits and the same thread polls.  A vx_ctx is not internally
  *    synchronised; internal HIP streams are invisible to the caller.
+ *    Separate contexts (e.g. one per torrent) share nothing but the device
+ *    and may be driven from different threads concurrently
+ *    (tests/test_gpu_parity.py::test_two_contexts_two_threads).
  *  - Device entry points (vx_sha1_device_*) take device pointers and a HIP
  *    stream (hipStream_t passed as void*; NULL = the null stream) and only
  *    enqueue work: they return before the kernel finishes.

@@ -528,6 +528,48 @@ def test_verify_files_chunk_schedule(built, gpu, tmp_path, monkeypatch, chunk, r
     assert sub == want[3:n - 1]
 
 
+def test_two_contexts_two_threads(built, gpu):
+    """Several torrents at once: one context each (different piece lengths),
+    driven from two threads concurrently, async spawns and sync batches mixed.
+    Contexts share nothing but the device (error text is thread-local)."""
+    import threading
+
+    from vortex_amd.hash_pool import HashPool
+
+    failures = []
+
+    def run(seed, plen, n):
+        try:
+            rng = random.Random(seed)
+            bodies = [oracle.gen_piece(seed, i, plen if i % 7 else rng.randint(1, plen)) for i in range(n)]
+            want = [hashlib.sha1(b).digest() for b in bodies]
+            with HashPool(plen, slots=3, batch_pieces=16) as pool:
+                for rep in range(3):
+                    for i, b in enumerate(bodies):
+                        exp = want[i] if (i + rep) % 11 else bytes(20)
+                        pool.spawn(i, rep, bytearray(b), len(b), exp)
+                        if i % 9 == 0:
+                            pool.flush()
+                    pool.drain()
+                    got = {r.index: r for r in pool.try_iter() if r.conn_id == rep}
+                    assert sorted(got) == list(range(n))
+                    for i, r in got.items():
+                        assert r.digest == want[i] and r.hash_matched == bool((i + rep) % 11)
+                    matched, dig = pool.verify_batch(bodies, want)
+                    assert all(matched) and list(dig) == want
+        except Exception as e:  # reported on the main thread
+            failures.append(f"seed {seed}: {e!r}")
+
+    ts = [threading.Thread(target=run, args=(21, 65536 + 64, 150)),
+          threading.Thread(target=run, args=(22, 3 * 16384, 260))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=110)
+    assert not any(t.is_alive() for t in ts)
+    assert not failures, failures
+
+
 def test_api_misuse_and_lifecycle(built, gpu):
     """Errors are codes, never aborts: busy-state checks, bad rows, and
     destroy with work in flight (drains like the reference's scope join)."""
