@@ -40,7 +40,13 @@ __device__ __forceinline__ void rounds(State& s, const uint4 (&w)[20]) {
                 f = VX_PAR(b, c, d);
                 k = 0xCA62C1D6u;
             }
+#ifdef VX_ROUND_X
+            uint32_t x = e + k + wq[j];
+            asm("" : "+v"(x));  // keep LLVM from reassociating: a' = add3(rotl5(a), f, x)
+            const uint32_t tmp = vx::rotl(a, 5) + f + x;
+#else
             const uint32_t tmp = vx::rotl(a, 5) + f + e + k + wq[j];
+#endif
             e = d;
             d = c;
             c = vx::rotl(b, 30);
