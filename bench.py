@@ -130,11 +130,15 @@ def e2e_rate(plen: int, n: int = 8192):
     with HashPool(plen, slots=4, slot_bytes=256 << 20, batch_pieces=1024) as pool:
         pool.register_buffer(buf)
         check(lib().vx_verify_batch(pool._h, ptrs, lens, exp, 256, matched, digests), "warm")
-        t0 = time.perf_counter()
-        check(lib().vx_verify_batch(pool._h, ptrs, lens, exp, n, matched, digests), "vx_verify_batch")
-        el = time.perf_counter() - t0
+        runs = []  # three timed calls (one 2 GiB call is ~40 ms); the median is reported
+        for _ in range(3):
+            ctypes.memset(matched, 0, n)
+            t0 = time.perf_counter()
+            check(lib().vx_verify_batch(pool._h, ptrs, lens, exp, n, matched, digests), "vx_verify_batch")
+            runs.append(time.perf_counter() - t0)
+            assert matched.raw[:n] == b"\x01" * n
         pool.unregister_buffer(buf)
-    assert matched.raw[:n] == b"\x01" * n
+    el = sorted(runs)[1]
     # plain pinned H2D copy of the same byte count, for context (PCIe Gen5 x16)
     host = torch.empty(n * plen, dtype=torch.uint8, pin_memory=True)
     dev_t = torch.empty(n * plen, dtype=torch.uint8, device="cuda")
@@ -146,8 +150,9 @@ def e2e_rate(plen: int, n: int = 8192):
     h2d = n * plen / (time.perf_counter() - t1) / GiB
     del dev_t, host
     return {"value": round(n * plen / el / GiB, 3), "unit": "GiB/s", "pinned_h2d_copy_GiBps": round(h2d, 2),
+            "runs_GiBps": [round(n * plen / r / GiB, 2) for r in runs],
             "sample": f"{n} x {plen // 1024} KiB from a registered host mmap via vx_verify_batch "
-                      f"(H2D + kernel + D2H), {el * 1e3:.1f} ms"}
+                      f"(H2D + kernel + D2H), median of 3 calls, {el * 1e3:.1f} ms"}
 
 
 def main() -> int:
