@@ -528,6 +528,68 @@ def test_verify_files_chunk_schedule(built, gpu, tmp_path, monkeypatch, chunk, r
     assert sub == want[3:n - 1]
 
 
+@pytest.mark.parametrize("seed", [101, 202, 303])
+def test_random_mix_all_paths(built, gpu, seed):
+    """Randomised batches through every host path, against hashlib: lengths
+    mix empty, sub-block, the 55/56/64 padding edges, 16-300 KiB and 1-3 MiB
+    pieces (so the whole-piece, gather and chunk paths all run), with random
+    mismatches; then the device ragged kernel (planner hint, both orders)."""
+    import mmap
+
+    import torch
+
+    from vortex_amd import device as vdev
+    from vortex_amd.hash_pool import HashPool
+
+    rng = random.Random(seed)
+    edges = [0, 1, 55, 56, 63, 64, 65, 119, 120, 128]
+    lens = []
+    for _ in range(rng.randint(40, 90)):
+        r = rng.random()
+        if r < 0.25:
+            lens.append(rng.choice(edges) + 64 * rng.randint(0, 3))
+        elif r < 0.8:
+            lens.append(rng.randint(16384, 300000))
+        else:
+            lens.append(rng.randint(1 << 20, 3 << 20))
+    bodies = [oracle.gen_piece(seed, i, L) for i, L in enumerate(lens)]
+    want = [hashlib.sha1(b).digest() for b in bodies]
+    exp = [w if rng.random() > 0.1 else bytes(20) for w in want]
+    maxlen = max(lens)
+    # one registered mmap holding every piece 16-byte aligned (the gather and
+    # chunk paths), and plain bytes objects (the staged path)
+    offs, o = [], 0
+    for L in lens:
+        offs.append(o)
+        o += (L + 15) // 16 * 16 + 16
+    mm = mmap.mmap(-1, max(o, 16))
+    for off, b in zip(offs, bodies):
+        mm[off:off + len(b)] = b
+    views = [memoryview(mm)[off:off + L] for off, L in zip(offs, lens)]
+    with HashPool(maxlen, slots=3, batch_pieces=32) as pool:
+        assert pool.sha1_batch(bodies) == want
+        pool.register_buffer(mm)
+        matched, dig = pool.verify_batch(views, exp)
+        assert dig == want and matched == [e == w for e, w in zip(exp, want)]
+        for i, v in enumerate(views if seed % 2 else bodies):
+            pool.spawn(i, seed, v, lens[i], exp[i])
+            if i % 13 == 0:
+                pool.flush()
+        pool.drain()
+        got = {r.index: r for r in pool.try_iter()}
+        assert sorted(got) == list(range(len(lens)))
+        for i, r in got.items():
+            assert r.digest == want[i] and r.hash_matched == (exp[i] == want[i])
+        del views
+        pool.unregister_buffer(mm)
+    d, doffs, dlens = _ragged_upload(torch, gpu, bodies)
+    for order in (None, vdev.length_order(lens).to(gpu)):
+        out, _ = vdev.sha1_ragged(d, doffs, dlens, order=order, plan=vdev.ragged_plan(lens))
+        torch.cuda.synchronize()
+        raw = out.cpu().numpy().tobytes()
+        assert [raw[20 * i:20 * i + 20] for i in range(len(lens))] == want
+
+
 def test_two_contexts_two_threads(built, gpu):
     """Several torrents at once: one context each (different piece lengths),
     driven from two threads concurrently, async spawns and sync batches mixed.
