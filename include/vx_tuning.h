@@ -5,7 +5,9 @@
  *   0 = default, 1 = lane-per-piece (one wave per 64 pieces does loads,
  *   schedule and rounds), 2 = producer/consumer split (a load+schedule wave
  *   feeds a rounds-only wave through an LDS ring), 3 / 4 = split with a 2- / 3-slot
- *   LDS ring (A/B of the ring protocol; 2 uses the default ring).
+ *   LDS ring (A/B of the ring protocol; 2 uses the default ring), 5 = split
+ *   with one pair per CU (ragged only; what the planner picks for batches
+ *   bound by their longest chain).
  */
 #ifndef VX_TUNING_H
 #define VX_TUNING_H
@@ -27,8 +29,8 @@ uint64_t vx_tuning_chunk_rounds(const struct vx_ctx* ctx);
  * buffers (async / batch slots). */
 uint64_t vx_tuning_gather_tiles(const struct vx_ctx* ctx);
 /* The kernel vx_sha1_device_ragged_hint runs for a batch of n pieces whose
- * longest is max_len bytes, total_len bytes in all: 1 = lane, 2 = split
- * (host-only). */
+ * longest is max_len bytes, total_len bytes in all: 1 = lane, 2 = split,
+ * 5 = split with one pair per CU (host-only). */
 int vx_tuning_plan_ragged(uint32_t n, uint32_t max_len, uint64_t total_len);
 /* The file re-verify's round boundaries for a window whose longest piece is
  * L bytes with chunk C (head/tail: ramp the first / last C bytes down to

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdint.h>
 
 #include "sha1_device.hpp"
@@ -721,12 +722,21 @@ __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
     }
 }
 
+// wide: unused dynamic LDS on top of the ring (60 KiB + 40 KiB > half of a
+// CU's 160 KiB), so each CU holds one pair.  On a chain-bound batch the pairs
+// hashing the longest pieces then keep their CU to themselves: config 3 56.8
+// -> 53.4 ms (282 -> 300 GiB/s), the rest of its 16 GiB still done in time
+// at half the split kernel's throughput.
+constexpr uint32_t kWidePadLds = 40 * 1024;
+
 template <int S>
 hipError_t launch_ragged_split_s(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens,
                                  const uint32_t* order, uint32_t n, uint8_t* digests, const uint8_t* expected,
-                                 uint8_t* matched, hipStream_t stream, const uint32_t* exp_index) {
+                                 uint8_t* matched, hipStream_t stream, const uint32_t* exp_index,
+                                 bool wide = false) {
     const uint32_t blocks = (n + 63) / 64;
-    hipLaunchKernelGGL((sha1_ragged_split_kernel<false, S>), dim3(blocks), dim3(kPairBlock), 0, stream, base,
+    hipLaunchKernelGGL((sha1_ragged_split_kernel<false, S>), dim3(blocks), dim3(kPairBlock),
+                       wide ? kWidePadLds : 0u, stream, base,
                        offsets, lens, order, n, digests, expected, matched, exp_index, nullptr, nullptr, nullptr,
                        nullptr);
     return hipGetLastError();
@@ -808,12 +818,16 @@ namespace vx {
 // (config 2 and config 3 measurements, §3.5: the lane kernel's VALU-bound
 // rate and per-block chain, the split kernel's).  Config 3's 4 MiB pieces make
 // it chain-bound: 77 ms lane vs 57 ms split, though it has 283,648 pieces.
+//
+// Split batches whose whole-chip work at HALF the split throughput (one pair
+// per CU) is still at most half their longest chain run wide (kSplitWide).
 int plan_ragged(uint32_t n, uint64_t max_len, uint64_t total_len) {
     (void)n;
     const double blocks = (double)((max_len + 9 + 63) / 64);
     const double lane = std::max((double)total_len / 3.4e12, blocks * 1.18e-6);
     const double split = std::max((double)total_len / 2.5e12, blocks * 0.87e-6);
-    return lane < split ? kUniformLane : kUniformSplit;
+    if (lane < split) return kUniformLane;
+    return (double)total_len / 1.25e12 <= 0.5 * blocks * 0.87e-6 ? kSplitWide : kUniformSplit;
 }
 
 // variant 0 without a plan: the split kernel.  A batch whose lengths really
@@ -829,6 +843,9 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
         return launch_ragged_split_s<2>(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
     if (variant == kSplitRing3)
         return launch_ragged_split_s<3>(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
+    if (variant == kSplitWide)
+        return launch_ragged_split_s<kSplitSlots>(base, offsets, lens, order, n, digests, expected, matched, stream,
+                                                  exp_index, true);
     return launch_ragged_split(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
 }
 }  // namespace vx

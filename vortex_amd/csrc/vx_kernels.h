@@ -13,7 +13,16 @@ constexpr int kPairBlock = 128;  // split kernel: consumer wave + producer wave
 
 // Uniform-batch kernel variants (vx_tuning.h): 0 = default (best measured),
 // 1 = lane-per-piece (one wave does everything), 2 = producer/consumer split.
-enum UniformVariant { kUniformDefault = 0, kUniformLane = 1, kUniformSplit = 2, kSplitRing2 = 3, kSplitRing3 = 4 };
+// kSplitWide: the split kernel with one pair per CU (padded LDS), for
+// batches bound by their longest chain with room to spare (plan_ragged).
+enum UniformVariant {
+    kUniformDefault = 0,
+    kUniformLane = 1,
+    kUniformSplit = 2,
+    kSplitRing2 = 3,
+    kSplitRing3 = 4,
+    kSplitWide = 5
+};
 // LDS ring slots of the split kernels (sha1_kernels.hip "Ring protocol").
 // 3: the producer runs two blocks ahead and the consumer prefetches the next
 // block into registers while compressing (config 5 geometry 28.1 -> 26.6 ms,
@@ -32,8 +41,9 @@ hipError_t launch_uniform_split(const uint8_t* base, uint64_t stride, uint32_t l
                                 const uint8_t* expected, uint8_t* matched, hipStream_t stream,
                                 const uint32_t* exp_index = nullptr);
 
-// Lane (kUniformLane) or split (kUniformSplit) for a ragged batch, from its
-// longest piece and total bytes.
+// Lane (kUniformLane), split (kUniformSplit) or split with one pair per CU
+// (kSplitWide) for a ragged batch, from its longest piece and total bytes
+// (DESIGN.md §3.4).
 int plan_ragged(uint32_t n, uint64_t max_len, uint64_t total_len);
 
 hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uint32_t* lens, const uint32_t* order,
