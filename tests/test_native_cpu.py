@@ -14,15 +14,17 @@ from conftest import ROOT
 SRC = os.path.join(ROOT, "tests", "native", "readers_stress.cpp")
 
 
-@pytest.mark.parametrize("sanitize", [False, True])
+@pytest.mark.parametrize("sanitize", [None, "thread", "address,undefined"])
 def test_reader_pool_generations(tmp_path, sanitize):
     if shutil.which("g++") is None:
         pytest.skip("g++ not available")
-    exe = tmp_path / ("rs_tsan" if sanitize else "rs")
+    exe = tmp_path / ("rs_" + (sanitize or "plain").replace(",", "_"))
     cmd = ["g++", "-O1", "-g", "-std=c++17", "-I" + os.path.join(ROOT, "include"),
            "-I" + os.path.join(ROOT, "vortex_amd", "csrc"), SRC, "-o", str(exe), "-lpthread"]
     if sanitize:
-        cmd.insert(1, "-fsanitize=thread")
+        cmd.insert(1, "-fsanitize=" + sanitize)
+        if "undefined" in sanitize:
+            cmd.insert(2, "-fno-sanitize-recover=undefined")
     subprocess.run(cmd, check=True)
     env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1 exitcode=66")
     out = subprocess.run([str(exe), str(tmp_path / "scratch.bin"), "1500", "6"], capture_output=True, text=True,
