@@ -1,7 +1,8 @@
 """CPU tests of host-side native code (no GPU): the pread pool behind
 vx_verify_files (vortex_amd/csrc/vx_files.hpp), stressed with back-to-back
-generations whose item vector is rebuilt between runs, plain and under
-ThreadSanitizer (host code only, as the GPU pool allows)."""
+generations whose item vector is rebuilt between runs (and the pipelined
+start/wait form), plain, under ThreadSanitizer and under ASan+UBSan (host
+code only, as the GPU pool allows)."""
 import json
 import os
 import shutil
