@@ -393,8 +393,13 @@ int launch_slot_impl(vx_ctx* c, int si) {
     if (s.gtiles) {
         VX_HIP(hipMemcpyAsync(s.d_src, s.h_src, (size_t)n * 8, hipMemcpyHostToDevice, cs));
         VX_HIP(hipMemcpyAsync(s.d_tfirst, s.h_tfirst, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, cs));
-        hipError_t e =
-            vx::launch_gather(s.d_src, s.d_offsets, s.d_lens, s.d_tfirst, n, s.gtiles, s.d_arena, cs, c->gather_grid);
+        // Slots of long pieces (>= 2 MiB on average) hash with a few
+        // chain-bound pairs that barely touch HBM, so the gather may use 128
+        // workgroups: async 2 / 4 MiB pieces 39.8 -> 43.2 / 35.8 -> 39.6 GiB/s.
+        // With shorter pieces the hash kernels compete and 128 cost up to 10 %
+        // (1 MiB: -2 %).  VX_GATHER_GRID overrides.
+        const uint32_t grid = c->gather_grid ? c->gather_grid : (s.bytes >= (uint64_t)n << 21 ? 128u : 0u);
+        hipError_t e = vx::launch_gather(s.d_src, s.d_offsets, s.d_lens, s.d_tfirst, n, s.gtiles, s.d_arena, cs, grid);
         if (e != hipSuccess) return hip_fail(e, "gather launch");
         c->gather_tiles += s.gtiles;
     }
