@@ -860,3 +860,48 @@ def test_gather_batch_chunked(built, gpu, monkeypatch, chunk):
         matched0, dig0 = pool.verify_batch(pieces, exp)  # unregistered: whole-piece staged path
         assert _lib.lib().vx_tuning_chunk_rounds(pool._h) == 0
     assert matched0 == matched and dig0 == want
+
+
+def test_pool_growth_mid_flight(built, gpu):
+    """vortex's BufferPool grows by doubling when it runs dry, mapping new
+    buffers while earlier pieces are still being hashed (buf_pool.rs:108-132).
+    Registering the new buffers must work with pieces in flight, pieces from
+    old and new buffers may share a batch, and unregistering is refused
+    (VX_EBUSY) until every completion has been polled, then succeeds."""
+    import mmap
+
+    from vortex_amd import _lib
+    from vortex_amd.hash_pool import HashPool
+
+    pl = 256 * 1024
+    gens = [2, 2, 4, 8]  # pool sizes after each growth: 2 -> 4 -> 8 -> 16 buffers
+    bufs, want, got = [], {}, {}
+    with HashPool(pl, slots=2, batch_pieces=6, slot_bytes=8 << 20) as pool:
+        idx = 0
+        for g, extra in enumerate(gens):
+            for _ in range(extra):  # growth: map + register while earlier pieces are in flight
+                b = mmap.mmap(-1, pl)
+                pool.register_buffer(b)
+                bufs.append(b)
+            for b in bufs:  # one piece per buffer, old and new interleaved
+                p = oracle.gen_piece(0x6207, idx, pl - (idx % 3) * 1000)
+                b[:len(p)] = p
+                want[idx] = hashlib.sha1(p).digest()
+                pool.spawn(idx, g, memoryview(b)[:len(p)], len(p), want[idx] if idx % 5 else bytes(20))
+                idx += 1
+            pool.flush()
+            if g == 1:
+                assert pool.pending > 0
+                with pytest.raises(_lib.VxError) as e:
+                    pool.unregister_buffer(bufs[0])
+                assert e.value.code == _lib.VX_EBUSY
+            pool.drain()  # buffers are rewritten next generation: wait for this one's reads
+            for r in pool.try_iter():
+                got[r.index] = r
+        assert pool.pending == 0
+        for b in bufs:
+            pool.unregister_buffer(b)
+    assert sorted(got) == sorted(want)
+    for i, r in got.items():
+        assert r.digest == want[i], i
+        assert r.hash_matched == (i % 5 != 0), i
