@@ -157,6 +157,8 @@ struct vx_ctx {
     // open; vx_poll launches it once a slot frees.
     bool flush_pending = false;
     bool lazy_flush = true;  // VX_LAZY_FLUSH=0: flush always launches (A/B)
+    bool batch_sort = true;  // VX_BATCH_SORT=0: host batches in caller order, batch_pieces launches (A/B)
+    bool bulk = false;       // inside vx_*_batch: slots fill to capacity, not to batch_pieces
     std::deque<vx_completion> done;
     struct Reg {
         size_t len;
@@ -568,7 +570,7 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
     s->n = i + 1;
     s->bytes = off + std::max<uint32_t>(len, 1);
     c->pending++;
-    if (s->n >= c->cfg.batch_pieces) return launch_slot(c, si);
+    if (s->n >= c->cfg.batch_pieces && !c->bulk) return launch_slot(c, si);
     return 0;
 }
 
@@ -633,6 +635,7 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (const char* m = std::getenv("VX_GATHER")) c->gather = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_GATHER_GRID")) c->gather_grid = (uint32_t)std::atoi(m);
     if (const char* m = std::getenv("VX_LAZY_FLUSH")) c->lazy_flush = std::atoi(m) != 0;
+    if (const char* m = std::getenv("VX_BATCH_SORT")) c->batch_sort = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_BATCH_CHUNK")) c->batch_chunk = align_up(std::strtoull(m, nullptr, 0), kAlign);
     if (const char* m = std::getenv("VX_VERIFY_CHUNK"))
         c->verify_chunk = std::max<uint64_t>(4096, align_up(std::strtoull(m, nullptr, 0), 4096));
@@ -1293,10 +1296,21 @@ int batch_chunked_gather(vx_ctx* c, const uint32_t* lens, const uint8_t* expecte
     int rc = cp.open(n, expected, "batch");
     const Slot& s0 = c->slots[0];
     const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>(s0.cap, s0.arena_cap / C));
+    // Windows take the pieces longest first (stable, so equal lengths keep the
+    // caller's order).  Every round of a window is one C-byte chain whatever
+    // its lane count, and a window runs rounds up to its longest piece: with a
+    // few long pieces in every window, every window pays that whole chain
+    // while its late rounds carry a few MiB each.  Grouped, the long pieces
+    // share rounds that stay PCIe-bound and the short ones finish in one
+    // round (config 3 from host: DESIGN.md §6.4).
+    std::vector<uint32_t> order(n);
+    std::iota(order.begin(), order.end(), 0u);
+    if (c->batch_sort)
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return lens[x] > lens[y]; });
     for (uint64_t w0 = 0; w0 < n && !rc; w0 += W) {
         const uint64_t w1 = std::min<uint64_t>(n, w0 + W);
         uint64_t wmax = 0;
-        for (uint64_t i = w0; i < w1; ++i) wmax = std::max<uint64_t>(wmax, lens[i]);
+        for (uint64_t p = w0; p < w1; ++p) wmax = std::max<uint64_t>(wmax, lens[order[p]]);
         const uint64_t rounds = std::max<uint64_t>(1, (wmax + C - 1) / C);
         for (uint64_t k = 0; k < rounds && !rc; ++k) {
             const uint64_t a = k * C;
@@ -1308,9 +1322,13 @@ int batch_chunked_gather(vx_ctx* c, const uint32_t* lens, const uint8_t* expecte
             Slot& s = c->slots[si];
             reset_fill(s);
             uint32_t m = 0, tiles = 0;
-            for (uint64_t i = w0; i < w1; ++i) {
+            for (uint64_t p = w0; p < w1; ++p) {
+                const uint64_t i = order[p];
                 const uint64_t L = lens[i];
-                if (a >= L && !(a == 0 && L == 0)) continue;  // piece already finished
+                if (a >= L && !(a == 0 && L == 0)) {  // piece finished
+                    if (c->batch_sort) break;          // and so is every later (shorter) one
+                    continue;
+                }
                 const uint32_t clen = (uint32_t)std::min<uint64_t>(C, L - a);
                 s.h_offsets[m] = (uint64_t)m * C;
                 s.h_lens[m] = clen;
@@ -1379,11 +1397,26 @@ static int batch_impl(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* len
     // Completions are harvested by acquire_filling when it runs out of slots;
     // polling here between submits would only add event queries to the
     // launch path, so the queue is drained only when it grows large.
-    for (size_t i = 0; i < n; ++i) {
+    //
+    // Pieces go in longest first and each slot fills to its capacity rather
+    // than to batch_pieces (which vx_config_default sizes for max_piece_len
+    // pieces).  A slot's kernel lasts as long as its longest piece's chain,
+    // so in caller order a ragged batch put a long piece into almost every
+    // small slot: config 3 from plain host memory ran at 2.1 GiB/s
+    // (DESIGN.md §6.4).  Tags stay the caller's indices.
+    std::vector<uint32_t> order(n);
+    std::iota(order.begin(), order.end(), 0u);
+    if (c->batch_sort)
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return lens[x] > lens[y]; });
+    c->bulk = c->batch_sort;
+    for (size_t p = 0; p < n; ++p) {
+        const size_t i = order[p];
         rc = submit_impl(c, i, ptrs[i], lens[i], expected ? expected + i * 20 : nullptr);
-        if (rc) return rc;
-        if (c->done.size() >= 65536 && (rc = collect())) return rc;
+        if (!rc && c->done.size() >= 65536) rc = collect();
+        if (rc) break;
     }
+    c->bulk = false;
+    if (rc) return rc;
     if ((rc = vx_drain(c, 0))) return rc;
     if ((rc = collect())) return rc;
     if (got != n) return fail(VX_EDEVICE, "batch: lost completions");
