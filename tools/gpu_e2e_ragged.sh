@@ -9,6 +9,7 @@ for v in 1 0 1; do
   VX_BATCH_SORT=$v timeout -k 10 200 python -u tools/e2e_ragged.py >> $O/ab_sort.jsonl 2>> $O/ab.err || { echo FAIL; tail -5 $O/ab.err; exit 1; }
 done
 for v in 1 0; do
-  VX_BATCH_SORT=$v timeout -k 10 200 python -u tools/e2e_ragged.py --unregistered --reps 1 >> $O/ab_sort.jsonl 2>> $O/ab.err || { echo FAIL; tail -5 $O/ab.err; exit 1; }
+  VX_BATCH_SORT=$v timeout -k 10 200 python -u tools/e2e_ragged.py --scale 0.125 >> $O/ab_sort.jsonl 2>> $O/ab.err || { echo FAIL; tail -5 $O/ab.err; exit 1; }
 done
+VX_BATCH_SORT=1 timeout -k 10 200 python -u tools/e2e_ragged.py --unregistered --reps 1 >> $O/ab_sort.jsonl 2>> $O/ab.err || { echo FAIL; tail -5 $O/ab.err; exit 1; }
 cat $O/ab_sort.jsonl

@@ -1307,6 +1307,69 @@ int batch_chunked_gather(vx_ctx* c, const uint32_t* lens, const uint8_t* expecte
     std::iota(order.begin(), order.end(), 0u);
     if (c->batch_sort)
         std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return lens[x] > lens[y]; });
+    auto gather_copy = [&](uint32_t m, uint32_t tiles) {
+        return [&, m, tiles](Slot& sl, hipStream_t st) -> int {
+            if (hipMemcpyAsync(sl.d_src, sl.h_src, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
+                hipMemcpyAsync(sl.d_tfirst, sl.h_tfirst, (size_t)(m + 1) * 4, hipMemcpyHostToDevice, st) !=
+                    hipSuccess)
+                return fail(VX_EDEVICE, "batch: gather table H2D failed");
+            hipError_t e = vx::launch_gather(sl.d_src, sl.d_offsets, sl.d_lens, sl.d_tfirst, m, tiles, sl.d_arena, st,
+                                             c->gather_grid);
+            if (e != hipSuccess) return hip_fail(e, "batch: gather launch");
+            c->gather_tiles += tiles;
+            return 0;
+        };
+    };
+    if (c->batch_sort) {
+        // Streaming rounds: a piece takes a lane from its first chunk to its
+        // last, and new pieces (longest first) join any round until it holds
+        // `target` bytes.  So the short pieces ride along the long pieces'
+        // later rounds instead of queueing behind them, and no round is a
+        // C-byte chain that moves only a few MiB.
+        uint64_t total = 0;
+        for (size_t i = 0; i < n; ++i) total += lens[i];
+        const uint64_t max_rounds = std::max<uint64_t>(1, (n ? (uint64_t)lens[order[0]] + C - 1 : 0) / C);
+        // Spread evenly over the longest piece's rounds: a round is bound by
+        // max(its bytes over PCIe, one C-byte chain), and the batch cannot take
+        // fewer rounds than its longest piece has chunks.  (A uniform batch gets
+        // target = n*C: every piece in the first round, as a window would.)
+        const uint64_t target = std::max<uint64_t>(1, (total + max_rounds - 1) / max_rounds);
+        std::vector<std::pair<uint32_t, uint64_t>> act, keep;  // (piece, next offset)
+        size_t next = 0;
+        while (!rc && (!act.empty() || next < n)) {
+            const int si = cp.free_slot([] {});
+            if (si < 0) {
+                rc = si;
+                break;
+            }
+            Slot& s = c->slots[si];
+            reset_fill(s);
+            uint32_t m = 0, tiles = 0;
+            uint64_t bytes = 0;
+            keep.clear();
+            auto lane = [&](uint32_t i, uint64_t a) {
+                const uint64_t L = lens[i];
+                const uint32_t clen = (uint32_t)std::min<uint64_t>(C, L - a);
+                s.h_offsets[m] = (uint64_t)m * C;
+                s.h_lens[m] = clen;
+                s.h_pidx[m] = i;
+                s.h_poff[m] = a;
+                s.h_tlen[m] = L;
+                s.h_src[m] = clen ? reinterpret_cast<uint64_t>(dev[i] + a) : 0;
+                tiles += clen ? vx::gather_tiles(clen) : 0;
+                s.h_tfirst[m + 1] = tiles;
+                ++m;
+                bytes += clen;
+                if (a + clen < L) keep.emplace_back(i, a + clen);
+            };
+            const bool continues = !act.empty();
+            for (const auto& pa : act) lane(pa.first, pa.second);
+            while (next < n && m < W && (bytes < target || m == 0)) lane(order[next++], 0);
+            act.swap(keep);
+            rc = cp.round(si, m, continues, gather_copy(m, tiles));
+        }
+        return cp.finish(matched_out, digests_out, rc);
+    }
     for (uint64_t w0 = 0; w0 < n && !rc; w0 += W) {
         const uint64_t w1 = std::min<uint64_t>(n, w0 + W);
         uint64_t wmax = 0;
@@ -1341,17 +1404,7 @@ int batch_chunked_gather(vx_ctx* c, const uint32_t* lens, const uint8_t* expecte
                 ++m;
             }
             if (m == 0) continue;
-            rc = cp.round(si, m, k > 0, [&](Slot& sl, hipStream_t st) {
-                if (hipMemcpyAsync(sl.d_src, sl.h_src, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
-                    hipMemcpyAsync(sl.d_tfirst, sl.h_tfirst, (size_t)(m + 1) * 4, hipMemcpyHostToDevice, st) !=
-                        hipSuccess)
-                    return fail(VX_EDEVICE, "batch: gather table H2D failed");
-                hipError_t e = vx::launch_gather(sl.d_src, sl.d_offsets, sl.d_lens, sl.d_tfirst, m, tiles,
-                                                 sl.d_arena, st, c->gather_grid);
-                if (e != hipSuccess) return hip_fail(e, "batch: gather launch");
-                c->gather_tiles += tiles;
-                return 0;
-            });
+            rc = cp.round(si, m, k > 0, gather_copy(m, tiles));
         }
         cp.end_window();
     }
