@@ -905,3 +905,47 @@ def test_pool_growth_mid_flight(built, gpu):
     for i, r in got.items():
         assert r.digest == want[i], i
         assert r.hash_matched == (i % 5 != 0), i
+
+
+@pytest.mark.parametrize("sort", ["1", "0"])
+def test_ragged_host_batch_streaming(built, gpu, monkeypatch, sort):
+    """A shuffled ragged host batch (config 3's shape, scaled down) in one
+    registered mmap takes the chunked gather path.  Longest-first streaming
+    rounds (VX_BATCH_SORT=1) admit short pieces into the long
+    pieces' later rounds and small slots force the lane limit; caller-order
+    windows (=0) are the A/B baseline.  Both must give hashlib's digests and
+    the expected verdicts, moving each chunk exactly once; the same batch in
+    plain memory (whole-piece slots, longest first) must agree too."""
+    import mmap
+
+    from vortex_amd import _lib
+    from vortex_amd.hash_pool import HashPool
+
+    monkeypatch.setenv("VX_BATCH_SORT", sort)
+    rng = random.Random(31)
+    lens = [(1 << 20) + 48] * 3 + [1 << 20] * 2 + [200000 + 16 * k for k in range(30)] + [16384] * 700 + \
+        [0, 16, 64, 4096, 65536, 65552] + [16 * rng.randint(1, 4096) for _ in range(300)]
+    rng.shuffle(lens)
+    offs, o = [], 0
+    for L in lens:
+        offs.append(o)
+        o += (L + 15) // 16 * 16
+    buf = mmap.mmap(-1, max(o, 1))
+    np.frombuffer(buf, dtype=np.uint8)[:] = np.random.default_rng(32).integers(0, 256, len(buf), dtype=np.uint8)
+    mv = memoryview(buf)
+    pieces = [mv[a:a + L] for a, L in zip(offs, lens)]
+    want = [hashlib.sha1(p).digest() for p in pieces]
+    assert want[0] == oracle.sha1(bytes(pieces[0]))
+    exp = [w if i % 11 else bytes(20) for i, w in enumerate(want)]
+    with HashPool(max(lens), slots=3, slot_bytes=4 << 20) as pool:  # 64 lanes per round: lane limit binds
+        pool.register_buffer(buf)
+        t0 = _lib.lib().vx_tuning_gather_tiles(pool._h)
+        matched, dig = pool.verify_batch(pieces, exp)
+        tiles = _lib.lib().vx_tuning_gather_tiles(pool._h) - t0
+        dig2 = pool.sha1_batch(pieces)
+        pool.unregister_buffer(buf)
+        matched_plain, dig_plain = pool.verify_batch([bytes(p) for p in pieces], exp)  # whole-piece slots
+    assert dig == want and dig2 == want and dig_plain == want
+    assert matched == [i % 11 != 0 for i in range(len(lens))]
+    assert matched_plain == matched
+    assert tiles == sum((L + 65535) // 65536 for L in lens)  # each 64 KiB chunk gathered once
