@@ -144,7 +144,9 @@ int vx_drain(vx_ctx* ctx, uint32_t timeout_ms);
 uint64_t vx_pending(const vx_ctx* ctx);
 
 /* ---- synchronous host batches (bulk re-verify, torrent.rs:724-740) ----- */
-/* digests_out: n*20 bytes.  Pieces are pipelined through the slots. */
+/* digests_out: n*20 bytes.  Pieces are pipelined through the slots, longest
+ * first (ragged batches: DESIGN.md §6.4); outputs are always in the caller's
+ * order.  Pieces may be of any lengths up to max_piece_len. */
 int vx_sha1_batch(vx_ctx* ctx, const uint8_t* const* ptrs, const uint32_t* lens, size_t n, uint8_t* digests_out);
 /* expected: n*20 bytes; matched_out: n bytes of 0/1 (the Box<[bool]> of
  * torrent.rs:727-740); digests_out may be NULL. */
