@@ -197,6 +197,15 @@ def test_submit_errors(built, gpu):
         assert e.value.code == VX_ERANGE
         with pytest.raises(ValueError):
             pool.spawn(0, 0, bytearray(10), 10, bytes(19))
+    # A host batch with one over-long piece is refused before anything is
+    # queued, and the context stays usable (no pieces left behind).
+    with HashPool(1000) as pool:
+        good = [oracle.gen_piece(8, i, 900) for i in range(50)]
+        with pytest.raises(VxError) as e:
+            pool.sha1_batch(good[:20] + [bytes(2000)] + good[20:])
+        assert e.value.code == VX_ERANGE
+        assert pool.pending == 0
+        assert pool.sha1_batch(good) == [hashlib.sha1(p).digest() for p in good]
 
 
 def test_host_batches_ragged(built, gpu):

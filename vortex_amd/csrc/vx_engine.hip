@@ -74,6 +74,12 @@ struct DirectRun {
     uint64_t lo, hi;
 };
 
+struct StageCopy {
+    const uint8_t* src;  // unregistered caller bytes for stage [off, off + len)
+    uint64_t off;
+    uint32_t len;
+};
+
 struct Slot {
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
@@ -109,6 +115,8 @@ struct Slot {
     std::vector<uint64_t> tags;
     std::vector<Run> runs;
     std::vector<DirectRun> druns;
+    std::vector<StageCopy> staged;  // host batches: stage copies deferred to launch
+    uint64_t staged_bytes = 0;
     uint32_t n = 0;
     uint64_t bytes = 0;
     bool uniform = true;
@@ -282,6 +290,8 @@ void reset_fill(Slot& s) {
     s.tags.clear();
     s.runs.clear();
     s.druns.clear();
+    s.staged.clear();
+    s.staged_bytes = 0;
     s.n = 0;
     s.bytes = 0;
     s.gtiles = 0;
@@ -292,6 +302,41 @@ void reset_fill(Slot& s) {
 }
 
 int launch_slot_impl(vx_ctx* c, int si);
+
+// A host batch's unregistered pieces reach the pinned stage here, split by
+// bytes over up to 16 threads: one thread's memcpy (~10-13 GiB/s) bounded
+// config 3 from plain memory.  The caller's buffers stay
+// valid because vx_*_batch returns only after every slot has completed.
+void stage_copies(Slot& s) {
+    if (s.staged.empty()) return;
+    const uint64_t per = 16ull << 20;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const unsigned T = (unsigned)std::min<uint64_t>({16, hw, std::max<uint64_t>(1, s.staged_bytes / per)});
+    auto copy = [&s](size_t a, size_t b) {
+        for (size_t k = a; k < b; ++k) std::memcpy(s.h_stage + s.staged[k].off, s.staged[k].src, s.staged[k].len);
+    };
+    if (T <= 1) {
+        copy(0, s.staged.size());
+    } else {
+        // contiguous ranges of roughly staged_bytes / T each
+        std::vector<size_t> cut{0};
+        uint64_t acc = 0, next = s.staged_bytes / T;
+        for (size_t k = 0; k < s.staged.size() && cut.size() < T; ++k) {
+            acc += s.staged[k].len;
+            if (acc >= next) {
+                cut.push_back(k + 1);
+                next += s.staged_bytes / T;
+            }
+        }
+        cut.push_back(s.staged.size());
+        std::vector<std::thread> th;
+        for (size_t t = 1; t + 1 < cut.size(); ++t) th.emplace_back(copy, cut[t], cut[t + 1]);
+        copy(cut[0], cut[1]);
+        for (auto& x : th) x.join();
+    }
+    s.staged.clear();
+    s.staged_bytes = 0;
+}
 
 // Order slot si's H2D after the previously launched slot's (one PCIe stream
 // of copies across all slots).  Modes:
@@ -382,6 +427,7 @@ int launch_slot_impl(vx_ctx* c, int si) {
         return 0;
     }
     hipStream_t cs = c->h2d_mode == 3 ? c->copy_stream : s.stream;
+    stage_copies(s);
     if (int rc = chain_h2d(c, si)) return rc;
     for (const DirectRun& r : s.druns)
         VX_HIP(hipMemcpyAsync(s.d_arena + r.lo, r.host, r.hi - r.lo, hipMemcpyHostToDevice, cs));
@@ -536,7 +582,12 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
                 s->druns.push_back(DirectRun{data, off, off + len});
         } else {
             if (int rc = ensure_stage(*s)) return rc;
-            std::memcpy(s->h_stage + off, data, len);
+            if (c->bulk) {  // a host batch: copied in parallel at launch (stage_copies)
+                s->staged.push_back(StageCopy{data, off, len});
+                s->staged_bytes += len;
+            } else {
+                std::memcpy(s->h_stage + off, data, len);
+            }
             if (!s->runs.empty() && s->runs.back().hi == off)
                 s->runs.back().hi = off + len;
             else if (!s->runs.empty() && align_up(s->runs.back().hi, kAlign) == off)
@@ -1457,6 +1508,10 @@ static int batch_impl(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* len
     // so in caller order a ragged batch put a long piece into almost every
     // small slot: config 3 from plain host memory ran at 2.1 GiB/s
     // (DESIGN.md §6.4).  Tags stay the caller's indices.
+    for (size_t i = 0; i < n; ++i) {  // argument errors before anything is queued
+        if (lens[i] > c->cfg.max_piece_len) return fail(VX_ERANGE, "batch: piece longer than max_piece_len");
+        if (lens[i] && !ptrs[i]) return fail(VX_EINVAL, "batch: NULL piece pointer");
+    }
     std::vector<uint32_t> order(n);
     std::iota(order.begin(), order.end(), 0u);
     if (c->batch_sort)
@@ -1469,6 +1524,10 @@ static int batch_impl(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* len
         if (rc) break;
     }
     c->bulk = false;
+    // Deferred stage copies must not outlive this call (the caller's buffers
+    // are borrowed only until it returns): a slot left filling by an error
+    // copies them now, as an immediate submit would have.
+    if (rc && c->filling >= 0) stage_copies(c->slots[c->filling]);
     if (rc) return rc;
     if ((rc = vx_drain(c, 0))) return rc;
     if ((rc = collect())) return rc;
