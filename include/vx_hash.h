@@ -176,7 +176,15 @@ int64_t vx_verify_files_range(vx_ctx* ctx, const char* const* paths, const uint6
                               uint32_t piece_length, const uint8_t* expected, size_t n_pieces, size_t first,
                               size_t count, uint8_t* matched_out, uint32_t io_threads);
 
-/* ---- device-resident batches (the hot path; no context needed) -------- */
+/* ---- device-resident batches (the hot path; no context needed) --------
+ * These entries validate what they can see on the host — NULL pointers, the
+ * alignment of d_base and stride, stride >= len — and nothing that lives in
+ * device memory: d_offsets, d_lens and d_order are read only by the kernel,
+ * so a misaligned or out-of-range offset, a length running past the
+ * allocation or an order index >= n is NOT detected here and makes the
+ * kernel read (or fault on) memory outside the batch.  Callers that build
+ * the layout on the host check it there; the Python wrapper
+ * vortex_amd.device.sha1_ragged checks it on the device before launching. */
 /* Pieces i in [0,n) at d_base + i*stride, each len bytes.  Writes
  * d_digests[20*i..] (may be NULL) and, when d_expected is given,
  * d_matched[i] = (digest == d_expected[20*i..]) (0/1).  stride and d_base

@@ -28,6 +28,10 @@ uint64_t vx_tuning_chunk_rounds(const struct vx_ctx* ctx);
 /* 64 KiB tiles the context's gather kernel has pulled from registered host
  * buffers (async / batch slots). */
 uint64_t vx_tuning_gather_tiles(const struct vx_ctx* ctx);
+/* Fault injection for tests: after k more successful piece submits (async or
+ * inside a host batch), the next one fails with VX_ENOMEM without latching
+ * the context, as a failed pinned-stage allocation does.  k < 0 turns it off. */
+void vx_tuning_fail_submit_after(struct vx_ctx* ctx, int64_t k);
 /* The kernel vx_sha1_device_ragged_hint runs for a batch of n pieces whose
  * longest is max_len bytes, total_len bytes in all: 1 = lane, 2 = split,
  * 5 = split with one pair per CU (host-only). */

@@ -76,6 +76,116 @@ def bdecode(b: bytes, i: int = 0):
     return b[j + 1:j + 1 + n], j + 1 + n
 
 
+def fill_bytes(fill: dict) -> bytes:
+    """File contents from a fixture `fill` spec (also used by the tests)."""
+    if "byte" in fill:
+        return bytes([fill["byte"]]) * fill["len"]
+    if "text" in fill:
+        return fill["text"].encode() * fill["repeat"]
+    return bytes.fromhex(fill["hex"])
+
+
+def interval_segments(file_lens, pl):
+    """Piece -> [(file_idx, offset_in_file, len)] by intersecting each piece's
+    global byte range [p*pl, min((p+1)*pl, total)) with each file's global
+    range.  A geometric statement of the mapping, independent of the
+    FileStore walk (file_store.rs:126-160, 240-298) that oracle/ and the
+    engine restate; zero-length intersections are omitted."""
+    starts, acc = [], 0
+    for L in file_lens:
+        starts.append(acc)
+        acc += L
+    total = acc
+    out = []
+    for p in range((total + pl - 1) // pl):
+        lo, hi = p * pl, min((p + 1) * pl, total)
+        segs = []
+        for fi, (s, L) in enumerate(zip(starts, file_lens)):
+            a, b = max(lo, s), min(hi, s + L)
+            if a < b:
+                segs.append([fi, a - s, b - a])
+        out.append(segs)
+    return out
+
+
+def file_store_layouts():
+    """The reference's own FileStore layout tests and integration-test
+    geometries (file path order; see the fixture's `order_note`)."""
+    import random
+
+    def rnd(seed, n):
+        r = random.Random(seed)
+        return {"hex": bytes(r.getrandbits(8) for _ in range(n)).hex()}
+
+    fs = "bittorrent/src/file_store.rs"
+    small6 = [("f1.txt", {"byte": 1, "len": 64}), ("f2.txt", {"byte": 2, "len": 100}),
+              ("f3.txt", {"byte": 3, "len": 50}), ("f4.txt", {"byte": 4, "len": 20}),
+              ("f5.txt", {"byte": 5, "len": 10}), ("f6.txt", {"byte": 6, "len": 268})]
+    v2 = [("f1.txt", {"byte": 1, "len": 84}), ("f2.txt", {"byte": 2, "len": 114}),
+          ("f3.txt", {"byte": 3, "len": 134}), ("f4.txt", {"byte": 4, "len": 24})]
+    sub, length = 32, 282
+    v2_single = b"".join(bytes([i]) * sub for i in range(length // sub)) + bytes([length // sub]) * (length % sub)
+    L = [
+        ("basic_multifile_alinged", f"{fs}:567-576", 256,
+         [(f"test/file_{i}.txt", {"byte": i, "len": 1024}) for i in range(10)]),
+        ("small_multifile_misalinged", f"{fs}:578-591", 256, small6),
+        ("small_multifile_misalinged_files_and_subpiece", f"{fs}:593-611 (subpiece 35)", 256, small6),
+        ("multifile_not_multiple_of_piece_size", f"{fs}:613-626", 256,
+         [("f1.txt", {"byte": 1, "len": 64}), ("f2.txt", {"byte": 2, "len": 256}),
+          ("f3.txt", {"byte": 3, "len": 50}), ("f4.txt", {"byte": 4, "len": 20}),
+          ("f5.txt", {"byte": 5, "len": 10}), ("f6.txt", {"byte": 6, "len": 300})]),
+        ("multifile_misalinged_v2", f"{fs}:628-639", 64, v2),
+        ("multifile_misalinged_v3", f"{fs}:641-652", 64, v2),
+        ("multifile_misalinged", f"{fs}:654-663", 256,
+         [(f"test/file_{i}.txt", {"byte": i, "len": 800}) for i in range(10)]),
+        ("basic_single_file_aligned", f"{fs}:665-674 (random bytes; seeded here)", 256,
+         [("test_single.txt", rnd(665, 1024))]),
+        ("basic_single_file_aligned_unaligned_subpiece", f"{fs}:676-690 (random bytes; seeded here)", 256,
+         [("test_single.txt", rnd(676, 1024))]),
+        ("single_file_misaligned", f"{fs}:692-701 (random bytes; seeded here)", 256,
+         [("test_single.txt", rnd(692, 1354))]),
+        ("single_file_misaligned_v2", f"{fs}:703-722", 256, [("test_single.txt", {"hex": v2_single.hex()})]),
+        ("disk_operations_for_all_valid_piece_indices", f"{fs}:724-760", 256,
+         [("test/root/test_single.txt", {"byte": 1, "len": 10000})]),
+        ("basic_seeding", "bittorrent/tests/basic_seeding.rs:27-48 (piece length 16384*8)", 16384 * 8,
+         [("file2.txt", {"text": "BitTorrent Test Data!", "repeat": 200}),
+          ("subdir/file3.txt", {"byte": 42, "len": 16384 * 5000 + 20000})]),
+        ("chained_seeding", "bittorrent/tests/chained_seeding.rs:32-51 (piece length 16384)", 16384,
+         [("file1.txt", {"text": "Chained Seeding Test!", "repeat": 150}),
+          ("file2.txt", {"text": "Middle peer uploads while downloading!", "repeat": 250}),
+          ("subdir/file3.txt", {"byte": 99, "len": 20480})]),
+        ("pause_resume", "bittorrent/tests/pause_resume.rs:27-42 (piece length 16384)", 16384,
+         [("file2.txt", {"text": "BitTorrent Test Data!", "repeat": 200}),
+          ("subdir/file3.txt", {"byte": 42, "len": 16384 * 5000})]),
+        # Not reference tests: edge cases of the same walk that no reference
+        # test reaches (zero-length files, a file ending exactly on a piece
+        # boundary, many files inside one piece, a one-byte last piece).
+        ("extra_zero_length_and_boundaries", "extra (not a reference test)", 64,
+         [("a", {"byte": 0xA1, "len": 64}), ("b", {"byte": 0xB2, "len": 0}), ("c", {"byte": 0xC3, "len": 3}),
+          ("d", {"byte": 0xD4, "len": 0}), ("e", {"byte": 0xE5, "len": 61}), ("f", rnd(9, 130)),
+          ("g", {"byte": 0x07, "len": 1}), ("h", {"byte": 0x08, "len": 1}), ("i", {"byte": 0x09, "len": 0})]),
+        ("extra_many_tiny_files", "extra (not a reference test)", 1000,
+         [(f"t/{k:03d}", rnd(100 + k, (k * 37) % 50)) for k in range(120)] + [("t/zz", {"byte": 1, "len": 1})]),
+    ]
+    out = []
+    for name, src, pl, files in L:
+        datas = [fill_bytes(fill) for _, fill in files]
+        lens = [len(d) for d in datas]
+        data = b"".join(datas)
+        total = len(data)
+        n = (total + pl - 1) // pl
+        digests = [hashlib.sha1(data[i:i + pl]).digest() for i in range(0, total, pl)]
+        ent = {"name": name, "source": src, "piece_length": pl,
+               "files": [{"path": p, "len": ln, "fill": f} for (p, f), ln in zip(files, lens)],
+               "total": total, "num_pieces": n, "last_piece_len": total - (n - 1) * pl if n else 0,
+               "pieces_sha1_of_table": hashlib.sha1(b"".join(digests)).hexdigest()}
+        if n <= 64:
+            ent["pieces"] = [d.hex() for d in digests]
+            ent["segments"] = interval_segments(lens, pl)
+        out.append(ent)
+    return out
+
+
 def main(ref_root: str) -> None:
     fips = [
         {"name": "empty", "hex_input": "", "sha1": "da39a3ee5e6b4b0d3255bfef95601890afd80709"},
@@ -128,6 +238,13 @@ def main(ref_root: str) -> None:
 
     out = {"fips": fips, "million_a": million_a, "boundary_pattern": "byte[i] = (i*131 + 7) & 0xff",
            "boundary": boundary, "setup_test": setup_test, "setup_seeding_test": seeding, "synthetic": synth}
+    out["file_store_layouts_note"] = (
+        "The reference's FileStore tests (file_store.rs:567-760) and integration tests build the torrent with "
+        "lava_torrent's TorrentBuilder from a HashMap of files; the file order is the builder's, taken here as "
+        "path order (the same assumption as setup_seeding_test). Tests also run each layout in reverse order, "
+        "so the mapping is pinned whatever the order. `pieces` = hashlib over the concatenated files; "
+        "`segments` = a geometric interval intersection (independent of the FileStore walk).")
+    out["file_store_layouts"] = file_store_layouts()
 
     torrent_path = os.path.join(ref_root, "cli", "linux-mint.torrent")
     if os.path.exists(torrent_path):

@@ -1,0 +1,149 @@
+"""GPU: host-batch error paths and the multi-threaded stage copy.
+
+* A host batch that fails part way (here: an injected VX_ENOMEM at the k-th
+  submit, the non-latching error a failed pinned-stage allocation gives)
+  returns only after every slot that was reading the caller's buffers has
+  finished, and leaves nothing pending: vx_poll returns nothing, buffers can
+  be unregistered (no EBUSY) and the next batch is bit-exact.
+* Unregistered pieces of a host batch are copied into the pinned stage at
+  launch by up to 16 threads (stage_copies); slots of 64 MiB and more split
+  the copy, and the result must still be bit-exact.
+* register_buffer refuses read-only objects and unregisters by object.
+"""
+import hashlib
+import mmap
+import random
+
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("fail_at", [0, 1, 37, 150, 299])
+def test_batch_failure_part_way_leaves_clean_context(built, gpu, fail_at):
+    from vortex_amd._lib import VX_ENOMEM, VxError, lib
+    from vortex_amd.hash_pool import HashPool
+
+    rng = random.Random(fail_at)
+    plen = 100_000
+    n = 300
+    lens = [rng.choice([plen, plen, 64, 0, 4097, 77_777]) for _ in range(n)]
+    reg = mmap.mmap(-1, n * 100_352)  # registered pool: one region, pieces 16-byte aligned
+    pieces, keep = [], []
+    for i, L in enumerate(lens):
+        body = oracle.gen_piece(0xE1, i, L)
+        if i % 2:
+            off = i * 100_352
+            reg[off:off + L] = body
+            pieces.append(memoryview(reg)[off:off + L])
+        else:
+            pieces.append(bytearray(body))
+        keep.append(body)
+    want = [hashlib.sha1(b).digest() for b in keep]
+    # slot_bytes 1 MiB: ~10 pieces per slot, so several slots are in flight when the failure hits
+    with HashPool(plen, slots=3, batch_pieces=8, slot_bytes=1 << 20) as pool:
+        pool.register_buffer(reg)
+        lib().vx_tuning_fail_submit_after(pool._h, fail_at)
+        with pytest.raises(VxError) as e:
+            pool.verify_batch(pieces, want)
+        assert e.value.code == VX_ENOMEM
+        assert pool.pending == 0
+        assert pool.try_iter() == []
+        lib().vx_tuning_fail_submit_after(pool._h, -1)
+        matched, dig = pool.verify_batch(pieces, want)
+        assert matched == [True] * n and dig == want
+        pool.unregister_buffer(reg)  # nothing in flight: must not be EBUSY
+    # the failure also hits the async path without latching the context
+    with HashPool(plen, slots=2, batch_pieces=4) as pool:
+        lib().vx_tuning_fail_submit_after(pool._h, 3)
+        bufs = [bytearray(keep[i]) for i in range(6)]
+        for i in range(3):
+            pool.spawn(i, 0, bufs[i], len(bufs[i]), want[i])
+        with pytest.raises(VxError):
+            pool.spawn(3, 0, bufs[3], len(bufs[3]), want[3])
+        pool.spawn(3, 0, bufs[3], len(bufs[3]), want[3])
+        pool.drain()
+        got = {r.index: r.hash_matched for r in pool.try_iter()}
+        assert got == {0: True, 1: True, 2: True, 3: True}
+
+
+def test_stage_copy_threads_large_slots(built, gpu):
+    """Unregistered host batch through 96 MiB slots: every launch splits its
+    stage copy over several threads (>= 16 MiB per thread)."""
+    from vortex_amd.hash_pool import HashPool
+
+    rng = random.Random(7)
+    lens = [rng.choice([1 << 20, (1 << 20) - 13, 262_144, 16_384, 999]) for _ in range(400)]
+    pieces = [oracle.gen_piece(0x57A6, i, L) for i, L in enumerate(lens)]
+    bufs = [bytearray(p) for p in pieces]
+    want = [hashlib.sha1(p).digest() for p in pieces]
+    exp = list(want)
+    exp[123] = bytes(20)
+    with HashPool(1 << 20, slots=3, slot_bytes=96 << 20) as pool:
+        matched, dig = pool.verify_batch(bufs, exp)
+        assert dig == want
+        assert matched == [i != 123 for i in range(len(pieces))]
+        assert pool.sha1_batch(bufs) == want
+
+
+def test_register_buffer_object_semantics(built, gpu):
+    from vortex_amd.hash_pool import HashPool
+
+    with HashPool(4096) as pool:
+        with pytest.raises(ValueError):
+            pool.register_buffer(b"\0" * 8192)  # read-only: would pin a private copy
+        ba = bytearray(8192)
+        pool.register_buffer(ba)
+        with pytest.raises(ValueError):
+            pool.register_buffer(ba)
+        with pytest.raises(ValueError):
+            pool.unregister_buffer(bytearray(8192))  # a different object
+        body = oracle.gen_piece(1, 2, 4000)
+        ba[:4000] = body
+        pool.spawn(0, 0, memoryview(ba)[:4096], 4000, hashlib.sha1(body).digest())
+        pool.drain()
+        assert [r.hash_matched for r in pool.try_iter()] == [True]
+        pool.unregister_buffer(ba)
+        pool.register_buffer(ba)  # registrable again after unregistering
+        pool.unregister_buffer(ba)
+
+
+def test_ragged_layout_validation(built, gpu):
+    """device.sha1_ragged refuses layouts the kernels would read out of
+    bounds with (the raw C entries do not validate device metadata,
+    vx_hash.h), and hashes a valid layout bit-exactly."""
+    import torch
+
+    from vortex_amd import device as vdev
+
+    body = oracle.gen_piece(0xA1, 0, 4096)
+    data = torch.frombuffer(bytearray(body), dtype=torch.uint8).to(gpu)
+
+    def run(offs, lens, order=None, validate=True):
+        o = torch.tensor(offs, dtype=torch.int64, device=gpu)
+        ln = torch.tensor(lens, dtype=torch.int32, device=gpu)
+        od = torch.tensor(order, dtype=torch.int32, device=gpu) if order is not None else None
+        dig, _ = vdev.sha1_ragged(data, o, ln, order=od, validate=validate)
+        torch.cuda.synchronize()
+        return dig.cpu().numpy().tobytes()
+
+    offs, lens = [0, 16, 4000, 4096], [10, 4080, 96, 0]
+    want = b"".join(hashlib.sha1(body[o:o + L]).digest() for o, L in zip(offs, lens))
+    assert run(offs, lens) == want
+    assert run(offs, lens, order=[1, 2, 0, 3]) == want
+    assert run(offs, lens, validate=False) == want
+    for bad in ([0, 8], [0, -16]):  # misaligned, negative
+        with pytest.raises(ValueError):
+            run(bad, [1, 1])
+    with pytest.raises(ValueError):
+        run([0, 4080], [10, 17])  # ends at 4097 > 4096
+    with pytest.raises(ValueError):
+        run([0, 16], [1, -1])
+    with pytest.raises(ValueError):
+        run([0, 16], [1, 1], order=[0, 2])
+    with pytest.raises(ValueError):
+        run([0, 16], [1, 1], order=[0])
+    with pytest.raises(ValueError):
+        vdev.sha1_uniform(data, 2, 2049, stride=2064)  # 2064 + 2049 > 4096

@@ -155,3 +155,37 @@ def test_pool_verify_files_restatement(tmp_path):
         touches_bad = 6 in spans[i] or any(fi == 4 and off + ln > 30000 for fi, off, ln in
                                           oracle.piece_segments(i, sizes, pl))
         assert got[i] == (not touches_bad), i
+
+
+def _layout_ids(golden_path=os.path.join(os.path.dirname(__file__), "golden", "vectors.json")):
+    import json
+
+    with open(golden_path) as f:
+        return [e["name"] for e in json.load(f)["file_store_layouts"]]
+
+
+@pytest.mark.parametrize("name", _layout_ids())
+@pytest.mark.parametrize("reverse", [False, True])
+def test_reference_file_store_layouts(golden, tmp_path, name, reverse):
+    """The reference's own FileStore layouts (file_store.rs:567-760, the
+    integration-test geometries) through the oracle's restatement of the
+    walk (piece_segments, file_store.rs:240-298) and the C++ bulk re-verify
+    pool (torrent.rs:724-740): segments equal the geometric interval
+    intersection, every piece verifies, and one flipped byte fails exactly
+    the piece that holds it."""
+    from _layouts import flip_file_byte, flip_offset, interval_segments, materialize
+
+    e = next(x for x in golden["file_store_layouts"] if x["name"] == name)
+    paths, lens, data, exp = materialize(e, tmp_path, reverse=reverse)
+    pl, n = e["piece_length"], e["num_pieces"]
+    assert len(exp) == 20 * n and sum(lens) == e["total"]
+    assert oracle.piece_len(n - 1, n, pl, e["total"]) == e["last_piece_len"]
+    geo = e["segments"] if ("segments" in e and not reverse) else interval_segments(lens, pl)
+    for i in range(n) if n <= 64 else (0, 1, n // 2, n - 2, n - 1):
+        assert [list(s) for s in oracle.piece_segments(i, lens, pl)] == geo[i], i
+    assert oracle.pool_verify_files(paths, lens, pl, exp, threads=4) == [True] * n
+    if n <= 64:
+        assert all(oracle.check_piece_hash_sync(paths, lens, pl, i, exp[20 * i:20 * i + 20]) for i in range(n))
+    off = flip_offset(e)
+    flip_file_byte(paths, lens, off)
+    assert oracle.pool_verify_files(paths, lens, pl, exp, threads=4) == [i != off // pl for i in range(n)]

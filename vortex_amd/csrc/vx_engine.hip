@@ -12,15 +12,20 @@
 // metadata.  Pieces are appended to the filling slot at 256-byte aligned
 // offsets: pieces inside a registered (pinned) host range are pulled at launch
 // by one gather kernel through the range's device mapping (vx_gather.hip);
-// others are memcpy'd into the slot's pinned stage at submit and moved with
-// one H2D per contiguous run at launch.
+// others go through the slot's pinned stage and move with one H2D per
+// contiguous run at launch.  On the async path (vx_submit) the stage copy is
+// a memcpy at submit; inside a host batch (vx_*_batch) the copies are
+// deferred to launch and split over up to 16 short-lived threads
+// (stage_copies), and the call waits for every slot before it returns.
 // A launch is H2D(meta) → kernel → D2H(digests, verdicts) → event; slots on
 // different streams overlap copy and compute.  vx_poll harvests finished
-// slots without blocking.  No internal threads: like the reference's loop,
-// everything is driven from the caller's thread.
+// slots without blocking.  The async path has no internal threads: like the
+// reference's loop, it is driven from the caller's thread.  The file
+// re-verify runs a pread reader pool (vx_files.hpp) for the call's duration.
 #include <hip/hip_runtime.h>
 
 #include <fcntl.h>
+#include <sched.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -184,6 +189,10 @@ struct vx_ctx {
     uint64_t pending = 0;
     uint64_t seq = 0;
     int sticky = 0;
+    // Fault injection for tests (vx_tuning_fail_submit_after): the submit
+    // after this many more succeeds fails with VX_ENOMEM, the way a failed
+    // pinned-stage allocation does; < 0 = off.
+    int64_t fail_submit_after = -1;
 };
 
 namespace {
@@ -303,14 +312,28 @@ void reset_fill(Slot& s) {
 
 int launch_slot_impl(vx_ctx* c, int si);
 
+// CPUs this process may run on (the container's or cgroup's share, not the
+// machine's: hardware_concurrency reports every CPU of a large host).
+unsigned usable_cpus() {
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof(set), &set) == 0) {
+        const int n = CPU_COUNT(&set);
+        if (n > 0) return (unsigned)n;
+    }
+    return std::max(1u, std::thread::hardware_concurrency());
+}
+
 // A host batch's unregistered pieces reach the pinned stage here, split by
 // bytes over up to 16 threads: one thread's memcpy (~10-13 GiB/s) bounded
 // config 3 from plain memory.  The caller's buffers stay
-// valid because vx_*_batch returns only after every slot has completed.
+// valid because vx_*_batch returns only after every slot has completed (or,
+// on an error, after every in-flight slot has been waited for: abandon_batch).
+// A thread that cannot be created leaves its range to the calling thread, so
+// no exception crosses the C ABI.
 void stage_copies(Slot& s) {
     if (s.staged.empty()) return;
     const uint64_t per = 16ull << 20;
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    static const unsigned hw = usable_cpus();
     const unsigned T = (unsigned)std::min<uint64_t>({16, hw, std::max<uint64_t>(1, s.staged_bytes / per)});
     auto copy = [&s](size_t a, size_t b) {
         for (size_t k = a; k < b; ++k) std::memcpy(s.h_stage + s.staged[k].off, s.staged[k].src, s.staged[k].len);
@@ -330,8 +353,14 @@ void stage_copies(Slot& s) {
         }
         cut.push_back(s.staged.size());
         std::vector<std::thread> th;
-        for (size_t t = 1; t + 1 < cut.size(); ++t) th.emplace_back(copy, cut[t], cut[t + 1]);
+        th.reserve(cut.size());
+        size_t t = 1;
+        try {
+            for (; t + 1 < cut.size(); ++t) th.emplace_back(copy, cut[t], cut[t + 1]);
+        } catch (...) {  // std::system_error (EAGAIN) or bad_alloc: copy the rest here
+        }
         copy(cut[0], cut[1]);
+        for (size_t u = t; u + 1 < cut.size(); ++u) copy(cut[u], cut[u + 1]);
         for (auto& x : th) x.join();
     }
     s.staged.clear();
@@ -549,6 +578,8 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
     if (c->sticky) return c->sticky;
     if (!data && len) return fail(VX_EINVAL, "vx_submit: data is NULL");
     if (len > c->cfg.max_piece_len) return fail(VX_ERANGE, "vx_submit: piece longer than max_piece_len");
+    if (c->fail_submit_after >= 0 && c->fail_submit_after-- == 0)
+        return fail(VX_ENOMEM, "vx_submit: injected failure (vx_tuning_fail_submit_after)");
     const bool table = piece_row >= 0;
     int si = acquire_filling(c);
     if (si < 0) return si;
@@ -1439,10 +1470,7 @@ int batch_chunked_gather(vx_ctx* c, const uint32_t* lens, const uint8_t* expecte
             for (uint64_t p = w0; p < w1; ++p) {
                 const uint64_t i = order[p];
                 const uint64_t L = lens[i];
-                if (a >= L && !(a == 0 && L == 0)) {  // piece finished
-                    if (c->batch_sort) break;          // and so is every later (shorter) one
-                    continue;
-                }
+                if (a >= L && !(a == 0 && L == 0)) continue;  // piece finished
                 const uint32_t clen = (uint32_t)std::min<uint64_t>(C, L - a);
                 s.h_offsets[m] = (uint64_t)m * C;
                 s.h_lens[m] = clen;
@@ -1460,6 +1488,28 @@ int batch_chunked_gather(vx_ctx* c, const uint32_t* lens, const uint8_t* expecte
         cp.end_window();
     }
     return cp.finish(matched_out, digests_out, rc);
+}
+
+// A host batch failed part way (an argument or allocation error at some
+// submit, a failed launch, a device error).  The call borrows the caller's
+// buffers only until it returns, so every slot still reading them — a DMA or
+// the gather kernel in flight — is waited for, and every piece of the call
+// is dropped: the filling slot is discarded without its deferred stage
+// copies, completions already queued are cleared, and pending returns to 0
+// (batch_impl starts with nothing pending), so later batches, vx_poll and
+// vx_unregister_host_buffer see a clean context.
+void abandon_batch(vx_ctx* c) {
+    for (auto& s : c->slots)
+        if (s.state == Slot::INFLIGHT) (void)hipEventSynchronize(s.done);
+    for (auto& s : c->slots)
+        if (s.state != Slot::FREE) {
+            reset_fill(s);
+            s.state = Slot::FREE;
+        }
+    c->done.clear();
+    c->filling = -1;
+    c->flush_pending = false;
+    c->pending = 0;
 }
 }  // namespace
 
@@ -1524,15 +1574,11 @@ static int batch_impl(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* len
         if (rc) break;
     }
     c->bulk = false;
-    // Deferred stage copies must not outlive this call (the caller's buffers
-    // are borrowed only until it returns): a slot left filling by an error
-    // copies them now, as an immediate submit would have.
-    if (rc && c->filling >= 0) stage_copies(c->slots[c->filling]);
-    if (rc) return rc;
-    if ((rc = vx_drain(c, 0))) return rc;
-    if ((rc = collect())) return rc;
-    if (got != n) return fail(VX_EDEVICE, "batch: lost completions");
-    return 0;
+    if (!rc) rc = vx_drain(c, 0);
+    if (!rc) rc = collect();
+    if (!rc && got != n) rc = fail(VX_EDEVICE, "batch: lost completions");
+    if (rc) abandon_batch(c);
+    return rc;
 }
 
 int vx_sha1_batch(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, size_t n, uint8_t* digests_out) {
@@ -1673,6 +1719,9 @@ int vx_sha1_device_ragged_hint(const void* d_base, const uint64_t* d_offsets, co
 
 uint64_t vx_tuning_chunk_rounds(const vx_ctx* c) { return c ? c->chunk_rounds : 0; }
 uint64_t vx_tuning_gather_tiles(const vx_ctx* c) { return c ? c->gather_tiles : 0; }
+void vx_tuning_fail_submit_after(vx_ctx* c, int64_t k) {
+    if (c) c->fail_submit_after = k < 0 ? -1 : k;
+}
 size_t vx_tuning_chunk_schedule(uint64_t L, uint64_t C, int head, int tail, uint64_t* out, size_t max) {
     if (C < 4 || C % 4) return 0;
     const auto r = chunk_schedule(L, C, std::max(0, std::min(5, head)), std::max(0, std::min(5, tail)));

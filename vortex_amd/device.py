@@ -47,12 +47,20 @@ def sha1_uniform(data: torch.Tensor, n: int, piece_len: int, stride: Optional[in
     dev = data.device
     if want_digests and digests is None:
         digests = torch.empty((n, 20), dtype=torch.uint8, device=dev)
+    elif want_digests:
+        _req(digests, "digests")
+        if digests.numel() < 20 * n or digests.device != dev:
+            raise ValueError("digests must hold n*20 bytes on the data's device")
     if expected is not None:
         _req(expected, "expected")
-        if expected.numel() < 20 * n:
-            raise ValueError("expected must hold n*20 bytes")
+        if expected.numel() < 20 * n or expected.device != dev:
+            raise ValueError("expected must hold n*20 bytes on the data's device")
         if matched is None:
             matched = torch.empty((n,), dtype=torch.uint8, device=dev)
+        else:
+            _req(matched, "matched")
+            if matched.numel() < n or matched.device != dev:
+                raise ValueError("matched must hold n bytes on the data's device")
     rc = lib().vx_sha1_device_uniform_variant(
         data.data_ptr(), stride, piece_len, n,
         digests.data_ptr() if (want_digests and digests is not None) else None,
@@ -63,10 +71,39 @@ def sha1_uniform(data: torch.Tensor, n: int, piece_len: int, stride: Optional[in
     return (digests if want_digests else None), (matched if expected is not None else None)
 
 
+def _check_ragged_layout(data: torch.Tensor, offsets: torch.Tensor, lens: torch.Tensor,
+                         order: Optional[torch.Tensor]) -> None:
+    """The kernels trust their offsets (vx_hash.h: the raw device entries do
+    not validate device-resident metadata), so check here what an
+    out-of-range batch would otherwise turn into reads of arbitrary HBM:
+    every offset 16-byte aligned and >= 0, every length >= 0, every piece
+    inside `data`, and `order` a set of indices in [0, n).  One small
+    reduction on the device and one 4-value copy back (a sync)."""
+    n = offsets.numel()
+    if n == 0:
+        return
+    ends = offsets + lens.to(torch.int64)
+    stats = torch.stack([
+        (offsets & 15).ne(0).any().to(torch.int64),
+        offsets.min().lt(0).to(torch.int64) + lens.min().lt(0).to(torch.int64),
+        ends.max(),
+        (order.min().lt(0) | order.max().ge(n)).to(torch.int64) if order is not None else offsets.new_zeros(()),
+    ]).cpu().tolist()
+    if stats[0]:
+        raise ValueError("sha1_ragged: every offset must be a multiple of 16 (the kernels load 16 bytes per lane)")
+    if stats[1]:
+        raise ValueError("sha1_ragged: negative offset or length")
+    if stats[2] > data.numel():
+        raise ValueError(f"sha1_ragged: a piece ends at byte {stats[2]}, past the data tensor ({data.numel()} bytes)")
+    if stats[3]:
+        raise ValueError("sha1_ragged: order holds an index outside [0, n)")
+
+
 def sha1_ragged(data: torch.Tensor, offsets: torch.Tensor, lens: torch.Tensor,
                 order: Optional[torch.Tensor] = None, expected: Optional[torch.Tensor] = None,
                 digests: Optional[torch.Tensor] = None, matched: Optional[torch.Tensor] = None,
-                stream: Optional[torch.cuda.Stream] = None, variant: int = 0, plan=None):
+                stream: Optional[torch.cuda.Stream] = None, variant: int = 0, plan=None,
+                validate: bool = True):
     """Hash piece i = data[offsets[i] : offsets[i]+lens[i]] for all i.
 
     offsets: int64 device tensor (16-byte aligned values); lens: int32 device
@@ -75,22 +112,40 @@ def sha1_ragged(data: torch.Tensor, offsets: torch.Tensor, lens: torch.Tensor,
     plan: (max_len, total_bytes) of the batch, known on the host when it is
     laid out (see :func:`ragged_plan`); with variant 0 the engine then picks
     the kernel whose time bound is lower (vx_sha1_device_ragged_hint,
-    DESIGN.md §3.4)."""
+    DESIGN.md §3.4).
+    validate: check alignment and bounds of offsets/lens/order first (a
+    device reduction and a sync; see :func:`_check_ragged_layout`).  Pass
+    False only for a layout built by trusted code, e.g. a timed loop over a
+    batch that was validated once."""
     _req(data, "data")
     _req(offsets, "offsets", torch.int64)
     _req(lens, "lens", torch.int32)
     n = offsets.numel()
     if lens.numel() != n:
         raise ValueError("offsets and lens differ in length")
-    dev = data.device
-    if digests is None:
-        digests = torch.empty((n, 20), dtype=torch.uint8, device=dev)
-    if expected is not None:
-        _req(expected, "expected")
-        if matched is None:
-            matched = torch.empty((n,), dtype=torch.uint8, device=dev)
     if order is not None:
         _req(order, "order", torch.int32)
+        if order.numel() != n:
+            raise ValueError("order must hold n indices")
+    dev = data.device
+    for name, t in (("offsets", offsets), ("lens", lens), ("order", order), ("expected", expected),
+                    ("digests", digests), ("matched", matched)):
+        if t is not None and t.device != dev:
+            raise ValueError(f"{name} is on {t.device}, data on {dev}")
+    if validate:
+        _check_ragged_layout(data, offsets, lens, order)
+    if digests is None:
+        digests = torch.empty((n, 20), dtype=torch.uint8, device=dev)
+    elif digests.dtype != torch.uint8 or not digests.is_contiguous() or digests.numel() < 20 * n:
+        raise ValueError("digests must be a contiguous uint8 tensor of n*20 bytes")
+    if expected is not None:
+        _req(expected, "expected")
+        if expected.numel() < 20 * n:
+            raise ValueError("expected must hold n*20 bytes")
+        if matched is None:
+            matched = torch.empty((n,), dtype=torch.uint8, device=dev)
+        elif matched.dtype != torch.uint8 or not matched.is_contiguous() or matched.numel() < n:
+            raise ValueError("matched must be a contiguous uint8 tensor of n bytes")
     exp_p = expected.data_ptr() if expected is not None else None
     m_p = matched.data_ptr() if expected is not None else None
     order_p = order.data_ptr() if order is not None else None

@@ -93,7 +93,7 @@ class HashPool:
         self._next_tag = 0
         self._inflight: dict[int, tuple[int, int, Any, Any]] = {}
         self._cbuf = (vx_completion * 1024)()
-        self._registered: dict[int, Any] = {}
+        self._registered: dict[int, tuple[int, Any, Any]] = {}  # id(buf) -> (address, keep-alive, buf)
 
     # -- lifecycle ---------------------------------------------------------
     def close(self) -> None:
@@ -115,15 +115,26 @@ class HashPool:
 
     # -- buffer pinning (buf_pool.rs / buf_ring.rs AnonymousMmap) -----------
     def register_buffer(self, buf) -> None:
+        """Pin a pool buffer (an mmap, bytearray or numpy array) for direct
+        DMA.  Read-only objects such as ``bytes`` are refused: pinning them
+        would pin a private copy that no later piece points into.  The
+        registration is keyed by the object, so ``unregister_buffer`` must be
+        given the same object."""
+        mv = memoryview(buf)
+        if mv.readonly:
+            raise ValueError("register_buffer needs a writable buffer (e.g. an mmap or bytearray), not a read-only one")
+        if id(buf) in self._registered:
+            raise ValueError("buffer is already registered with this pool")
         addr, keep = _addr_of(buf)
-        n = memoryview(buf).nbytes
-        check(lib().vx_register_host_buffer(self._h, addr, n), "vx_register_host_buffer")
-        self._registered[addr] = keep
+        check(lib().vx_register_host_buffer(self._h, addr, mv.nbytes), "vx_register_host_buffer")
+        self._registered[id(buf)] = (addr, keep, buf)
 
     def unregister_buffer(self, buf) -> None:
-        addr, _ = _addr_of(buf)
-        check(lib().vx_unregister_host_buffer(self._h, addr), "vx_unregister_host_buffer")
-        self._registered.pop(addr, None)
+        ent = self._registered.get(id(buf))
+        if ent is None or ent[2] is not buf:
+            raise ValueError("buffer was not registered with this pool")
+        check(lib().vx_unregister_host_buffer(self._h, ent[0]), "vx_unregister_host_buffer")
+        del self._registered[id(buf)]
 
     # -- download path -------------------------------------------------------
     def spawn(self, index: int, conn_id: int, buffer, piece_len: int, expected_hash: Optional[bytes] = None) -> None:
