@@ -175,6 +175,43 @@ int64_t vx_verify_files(vx_ctx* ctx, const char* const* paths, const uint64_t* f
 int64_t vx_verify_files_range(vx_ctx* ctx, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
                               uint32_t piece_length, const uint8_t* expected, size_t n_pieces, size_t first,
                               size_t count, uint8_t* matched_out, uint32_t io_threads);
+/* In-process multi-GPU re-verify: vortex is one process with one event loop
+ * (event_loop.rs:385), so on a multi-GPU host it holds one context per GPU
+ * (vx_config.device) and hands them all to this call, which replaces the
+ * whole par_iter of torrent.rs:724-740.  Pieces [0, n_pieces) are split into
+ * nctx contiguous ranges (n_pieces/nctx each, the remainder to the last
+ * contexts — the rule of vortex_amd.shard.shard_range) and context k verifies
+ * range k on its own host thread with vx_verify_files_range, writing
+ * matched_out[first_k ..] in place.  io_threads is the total reader count,
+ * divided among the contexts (0 = default).  Contexts must be distinct and
+ * idle; they may share a device.  Returns the summed I/O-error count, or the
+ * first failing context's VX_E* code (vx_last_error names the context). */
+int64_t vx_verify_files_multi(vx_ctx* const* ctxs, size_t nctx, const char* const* paths,
+                              const uint64_t* file_lengths, size_t nfiles, uint32_t piece_length,
+                              const uint8_t* expected, size_t n_pieces, uint8_t* matched_out, uint32_t io_threads);
+
+/* ---- planning: where should a bulk verify run? (host-only, no GPU) -----
+ * One piece is one lane on the GPU and SHA-1 cannot be split inside a
+ * piece, so a few very long pieces are bound by one lane's chain (~0.81 us
+ * per 64-byte block, ~79 MB/s), while vortex's own rayon + `sha1` pool
+ * (torrent.rs:724-740) hashes one piece per core at ~2 GB/s.  This cost model
+ * (calibrated on MI355X) predicts both for n_pieces pieces of
+ * piece_length bytes (total_length in all, the last piece shorter) read from
+ * host memory or the page cache, so the caller can keep its own pool where it
+ * is faster (INTEGRATION.md "Where the GPU pays").  cpu_threads / cpu_thread_rate
+ * describe the caller's pool (0 = 16 threads / 2.2e9 B/s per thread, SHA-NI). */
+typedef struct vx_plan {
+    double gpu_s;               /* predicted e2e seconds of vx_verify_files / vx_verify_batch   */
+    double gpu_chain_s;         /* one piece's chain of compressions in one lane               */
+    double gpu_transfer_s;      /* all bytes over PCIe                                         */
+    double cpu_s;               /* predicted seconds of the caller's pool                      */
+    double piece_latency_s;     /* download path: submit-to-poll floor of one piece on the GPU */
+    double cpu_piece_latency_s; /* the same piece on one pool thread                           */
+    int32_t use_gpu;            /* 1 when 1.1 * gpu_s < cpu_s (near a tie, keep the CPU pool)  */
+    uint32_t _pad;
+} vx_plan;
+int vx_plan_verify(uint64_t n_pieces, uint32_t piece_length, uint64_t total_length, uint32_t cpu_threads,
+                   double cpu_thread_rate, vx_plan* out);
 
 /* ---- device-resident batches (the hot path; no context needed) --------
  * These entries validate what they can see on the host — NULL pointers, the

@@ -177,3 +177,66 @@ def test_chunk_schedule_properties(built, seed):
                 assert r[-1][1] <= q and r[-2][1] == q
         if L > 2 * C and (d == 0 or q < 64):
             assert all(ln == C for _, ln in r[:-1])
+
+
+def _plan(n, pl, total, threads=16, rate=2.0e9):
+    from vortex_amd import _lib
+
+    p = _lib.vx_plan()
+    rc = _lib.lib().vx_plan_verify(n, pl, total, threads, rate, ctypes.byref(p))
+    return rc, p
+
+
+def test_plan_verify_host(built):
+    """vx_plan_verify, host-only: the BASELINE re-verify
+    geometry goes to the GPU, a few very long pieces stay on the caller's
+    pool (one lane's chain), many long pieces go back to the GPU, and a much
+    larger CPU pool wins where its rate beats PCIe."""
+    from vortex_amd import _lib
+
+    MiB = 1 << 20
+    rc, p = _plan(1387, 2 * MiB, 2907832320)                 # config 5 (linux-mint geometry)
+    assert rc == 0 and p.use_gpu == 1
+    assert p.gpu_transfer_s > p.gpu_chain_s and p.gpu_s < p.cpu_s
+    rc, p = _plan(174, 16 * MiB, 174 * 16 * MiB)              # few long pieces: chain-bound
+    assert rc == 0 and p.use_gpu == 0 and p.gpu_chain_s > p.gpu_transfer_s
+    assert p.piece_latency_s > 0.15 > p.cpu_piece_latency_s    # past the loop's 150 ms CQE wait (torrent.rs:42)
+    rc, p = _plan(8192, 16 * MiB, 8192 * 16 * MiB)            # many long pieces: PCIe-bound again
+    assert rc == 0 and p.use_gpu == 1
+    rc, p = _plan(8192, 16 * MiB, 8192 * 16 * MiB, threads=128)
+    assert rc == 0 and p.use_gpu == 0                          # a 128-thread pool outruns PCIe
+    rc, p = _plan(8192, 256 * 1024, 8192 * 256 * 1024)         # bench e2e sample
+    assert rc == 0 and p.use_gpu == 1
+    # the last piece may be short; n must match the total
+    assert _plan(3, 1000, 2001)[0] == 0
+    assert _plan(3, 1000, 3001)[0] == _lib.VX_EINVAL
+    assert _plan(0, 1000, 0)[0] == 0
+    assert _lib.lib().vx_plan_verify(1, 0, 1, 16, 2e9, None) == _lib.VX_EINVAL
+    # monotone in the caller's pool
+    prev = None
+    for t in (1, 2, 4, 8, 16, 32, 64):
+        cpu = _plan(4096, 4 * MiB, 4096 * 4 * MiB, threads=t)[1].cpu_s
+        assert prev is None or cpu < prev
+        prev = cpu
+
+
+def test_plan_verify_matches_measured_grid(built):
+    """The planner against the crossover grid measured on one MI355X
+    (tools/crossover_grid.py -> profiles/r02/crossover/grid.json): the
+    decision equals the measured winner at every point, and the predicted
+    GPU time is within 20 % of the measured one."""
+    import json
+
+    with open(os.path.join(ROOT, "profiles", "r02", "crossover", "grid.json")) as f:
+        grid = json.load(f)
+    MiB = 1 << 20
+    assert len(grid["points"]) >= 20
+    for pt in grid["points"]:
+        L = pt["piece_MiB"] * MiB
+        rc, p = _plan(pt["n"], L, pt["n"] * L, threads=grid["threads"])
+        assert rc == 0
+        assert p.use_gpu == (pt["winner"] == "gpu"), pt
+        assert abs(p.gpu_s / pt["gpu_s"] - 1) < 0.20, (pt, p.gpu_s)
+    for lp in grid["loop"]:  # download path: latency p50 ~ one piece's chain
+        rc, p = _plan(1, lp["piece_len"], lp["piece_len"])
+        assert abs(p.piece_latency_s * 1e3 / lp["latency_ms_p50"] - 1) < 0.15, lp

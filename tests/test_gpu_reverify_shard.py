@@ -105,3 +105,43 @@ def test_verify_files_sharded_ranks(built, gpu, tmp_path, world):
             if a < starts[k] + sizes[k] and b > starts[k] + lim:
                 lost.add(i)
     assert res["bad"] == len(lost)
+
+
+@pytest.mark.parametrize("nctx,pl", [(2, 256 * 1024), (3, 1 << 20), (3, 64 * 1024 + 64)])
+def test_verify_files_multi_contexts(built, gpu, tmp_path, nctx, pl):
+    """vx_verify_files_multi: the in-process multi-device form vortex (one
+    process, one event loop) would call — nctx contexts, all on this box's
+    device 0 here, each verifying its contiguous range on its own thread.
+    Equal to the one-context call and to the oracle, damaged files included;
+    the I/O-error count is the same as one context's."""
+    from vortex_amd._lib import VX_EINVAL, VxError
+    from vortex_amd.hash_pool import HashPool, verify_files_multi
+
+    sizes = [3, 4 * pl + 17, 2 * pl, 0, 3 * pl - 5, pl + 1, 64, 9 * pl + pl // 2]
+    paths, exp = _torrent(tmp_path, pl, sizes, 23 + nctx)
+    n = len(exp) // 20
+    _damage(paths, pl)
+    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
+    assert not all(want) and any(want)
+    pools = [HashPool(pl, slots=2 + k % 2, slot_bytes=(2 + k) << 20) for k in range(nctx)]
+    try:
+        one, bad_one = pools[0].verify_files(paths, sizes, pl, exp)
+        assert one == want
+        for io in (0, 1, 7):
+            got, bad = verify_files_multi(pools, paths, sizes, pl, exp, io_threads=io)
+            assert got == want and bad == bad_one, io
+        # fewer pieces than contexts: the first contexts get empty ranges
+        tiny = tmp_path / "tiny.bin"
+        tiny.write_bytes(oracle.gen_piece(5, 5, pl + 1))
+        texp = hashlib.sha1(tiny.read_bytes()[:pl]).digest() + bytes(20)  # piece 1 mismatches
+        got, bad = verify_files_multi(pools, [str(tiny)], [pl + 1], pl, texp)
+        assert got == [True, False] and bad == 0
+        with pytest.raises(VxError) as e:
+            verify_files_multi([pools[0], pools[0]], paths, sizes, pl, exp)
+        assert e.value.code == VX_EINVAL
+        with pytest.raises(VxError) as e:  # n_pieces inconsistent with the files
+            verify_files_multi(pools, paths, sizes, pl, exp + bytes(20))
+        assert e.value.code == VX_EINVAL
+    finally:
+        for p in pools:
+            p.close()

@@ -34,11 +34,11 @@ EXPORTS = (
     "vx_abi_version", "vx_last_error", "vx_strerror", "vx_device_count", "vx_config_default",
     "vx_create", "vx_destroy", "vx_register_host_buffer", "vx_unregister_host_buffer",
     "vx_submit", "vx_flush", "vx_poll", "vx_drain", "vx_pending", "vx_set_piece_table", "vx_submit_piece",
-    "vx_sha1_batch", "vx_verify_batch", "vx_verify_files", "vx_verify_files_range",
+    "vx_sha1_batch", "vx_verify_batch", "vx_verify_files", "vx_verify_files_range", "vx_verify_files_multi",
     "vx_sha1_device_uniform", "vx_sha1_device_ragged", "vx_sha1_device_ragged_hint", "vx_sort_order",
     "vx_synth_fill", "vx_sha1_device_uniform_variant", "vx_sha1_device_ragged_variant",
     "vx_tuning_chunk_rounds", "vx_tuning_gather_tiles", "vx_tuning_plan_ragged", "vx_tuning_chunk_schedule",
-    "vx_tuning_fail_submit_after",
+    "vx_tuning_fail_submit_after", "vx_plan_verify",
 )
 
 
@@ -56,6 +56,12 @@ class vx_completion(ctypes.Structure):
 class vx_config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("max_piece_len", ctypes.c_uint32), ("batch_pieces", ctypes.c_uint32),
                 ("slots", ctypes.c_uint32), ("slot_bytes", ctypes.c_uint64)]
+
+
+class vx_plan(ctypes.Structure):
+    _fields_ = [("gpu_s", ctypes.c_double), ("gpu_chain_s", ctypes.c_double), ("gpu_transfer_s", ctypes.c_double),
+                ("cpu_s", ctypes.c_double), ("piece_latency_s", ctypes.c_double),
+                ("cpu_piece_latency_s", ctypes.c_double), ("use_gpu", ctypes.c_int32), ("_pad", ctypes.c_uint32)]
 
 
 _lib = None
@@ -87,6 +93,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "vx_verify_files": ([vp, vp, vp, c.c_size_t, c.c_uint32, vp, c.c_size_t, vp, c.c_uint32], c.c_int64),
         "vx_verify_files_range": ([vp, vp, vp, c.c_size_t, c.c_uint32, vp, c.c_size_t, c.c_size_t, c.c_size_t, vp,
                                    c.c_uint32], c.c_int64),
+        "vx_verify_files_multi": ([vp, c.c_size_t, vp, vp, c.c_size_t, c.c_uint32, vp, c.c_size_t, vp, c.c_uint32],
+                                  c.c_int64),
         "vx_sha1_device_uniform": ([vp, c.c_uint64, c.c_uint32, c.c_uint32, vp, vp, vp, vp], c.c_int),
         "vx_sha1_device_ragged": ([vp, vp, vp, vp, c.c_uint32, vp, vp, vp, vp], c.c_int),
         "vx_sha1_device_ragged_hint": ([vp, vp, vp, vp, c.c_uint32, c.c_uint32, c.c_uint64, vp, vp, vp, vp],
@@ -98,6 +106,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "vx_tuning_chunk_rounds": ([vp], c.c_uint64),
         "vx_tuning_gather_tiles": ([vp], c.c_uint64),
         "vx_tuning_fail_submit_after": ([vp, c.c_int64], None),
+        "vx_plan_verify": ([c.c_uint64, c.c_uint32, c.c_uint64, c.c_uint32, c.c_double, c.POINTER(vx_plan)], c.c_int),
         "vx_tuning_plan_ragged": ([c.c_uint32, c.c_uint32, c.c_uint64], c.c_int),
         "vx_tuning_chunk_schedule": ([c.c_uint64, c.c_uint64, c.c_int, c.c_int, c.POINTER(c.c_uint64), c.c_size_t],
                                      c.c_size_t),

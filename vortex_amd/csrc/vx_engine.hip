@@ -30,6 +30,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -1661,6 +1662,57 @@ int64_t vx_verify_files(vx_ctx* c, const char* const* paths, const uint64_t* fil
                                  matched_out, io_threads);
 }
 
+// In-process multi-device re-verify: vortex is ONE process
+// with one event loop (event_loop.rs:385), so where torch.distributed would
+// run one process per GPU, a Rust caller holds one context per GPU and this
+// call splits [0, n_pieces) across them by the same contiguous rule as
+// vortex_amd.shard.shard_range (n/nctx each, remainder to the last
+// contexts), one host thread per context.  Each thread runs
+// vx_verify_files_range on its context and writes its slice of matched_out
+// in place, so no merge step is needed.
+int64_t vx_verify_files_multi(vx_ctx* const* ctxs, size_t nctx, const char* const* paths,
+                              const uint64_t* file_lengths, size_t nfiles, uint32_t piece_length,
+                              const uint8_t* expected, size_t n_pieces, uint8_t* matched_out, uint32_t io_threads) {
+    if (!ctxs || nctx == 0 || nctx > 1024) return fail(VX_EINVAL, "vx_verify_files_multi: bad context list");
+    for (size_t k = 0; k < nctx; ++k) {
+        if (!ctxs[k]) return fail(VX_EINVAL, "vx_verify_files_multi: NULL context");
+        for (size_t j = 0; j < k; ++j)
+            if (ctxs[j] == ctxs[k]) return fail(VX_EINVAL, "vx_verify_files_multi: a context appears twice");
+    }
+    if (n_pieces && (!expected || !matched_out)) return fail(VX_EINVAL, "vx_verify_files_multi: bad argument");
+    const uint32_t total_io = io_threads ? io_threads : std::max(1u, std::min(16u, usable_cpus()));
+    const uint32_t per_ctx = std::max<uint32_t>(1, total_io / (uint32_t)nctx);
+    const size_t base = n_pieces / nctx, rem = n_pieces % nctx, extra_from = nctx - rem;
+    std::vector<int64_t> rcs(nctx, 0);
+    std::vector<std::string> errs(nctx);
+    auto run = [&](size_t k) {
+        const size_t first = k * base + (k > extra_from ? k - extra_from : 0);
+        const size_t count = base + (k >= extra_from ? 1 : 0);
+        rcs[k] = vx_verify_files_range(ctxs[k], paths, file_lengths, nfiles, piece_length, expected, n_pieces,
+                                       first, count, matched_out + first, per_ctx);
+        if (rcs[k] < 0) errs[k] = g_err;  // g_err is thread-local
+    };
+    std::vector<std::thread> th;
+    th.reserve(nctx);
+    size_t started = 1;
+    try {
+        for (; started < nctx; ++started) th.emplace_back(run, started);
+    } catch (...) {  // could not start a thread: run the rest on this one
+    }
+    run(0);
+    for (size_t k = started; k < nctx; ++k) run(k);
+    for (auto& t : th) t.join();
+    int64_t nbad = 0;
+    for (size_t k = 0; k < nctx; ++k) {
+        if (rcs[k] < 0) {
+            g_err = "context " + std::to_string(k) + ": " + errs[k];
+            return rcs[k];
+        }
+        nbad += rcs[k];
+    }
+    return nbad;
+}
+
 int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
                                    const void* d_expected, void* d_matched, void* stream, int variant) {
     if (n == 0) return 0;
@@ -1715,6 +1767,46 @@ int vx_sha1_device_ragged_hint(const void* d_base, const uint64_t* d_offsets, co
                                void* d_digests, const void* d_expected, void* d_matched, void* stream) {
     return vx_sha1_device_ragged_variant(d_base, d_offsets, d_lens, d_order, n, d_digests, d_expected, d_matched,
                                          stream, vx::plan_ragged(n, max_len, total_len));
+}
+
+// Host-only cost model of a bulk verify.  One piece is one
+// lane and SHA-1 is Merkle-Damgård, so a piece of L bytes is a chain of
+// blocks(L) dependent compressions at kChainBlock seconds each on the split
+// kernel, and the chunk pipeline (§6.3) adds a fixed setup and a cost per
+// round of C = 256 KiB; the bytes cross PCIe at kPcieRate.  The call takes
+// the larger of the two, plus a fraction of the smaller (they overlap, but
+// not perfectly).  The caller's pool: ceil(n / threads) rounds of one piece
+// per thread at cpu_thread_rate bytes/s (rayon runs one piece per task,
+// torrent.rs:724-740).  Fitted to the measured grid of tools/crossover_grid.py
+// (profiles/r02/crossover/grid.json: 22 points, 2-16 MiB x 64-4,096 pieces,
+// GPU predictions within 8 % but one point at 17 %); tests/test_abi.py checks
+// the fit and every decision against that file.  use_gpu asks for a 10 %
+// margin: near a tie the caller's own pool is the safe choice.
+int vx_plan_verify(uint64_t n_pieces, uint32_t piece_length, uint64_t total_length, uint32_t cpu_threads,
+                   double cpu_thread_rate, vx_plan* out) {
+    if (!out || piece_length == 0) return fail(VX_EINVAL, "vx_plan_verify: bad argument");
+    if (n_pieces != (total_length + piece_length - 1) / piece_length)
+        return fail(VX_EINVAL, "vx_plan_verify: n_pieces does not match total_length");
+    constexpr double kChainBlock = 0.81e-6, kPcieRate = 50.0 * (1ull << 30), kSetup = 3e-3, kRound = 0.6e-3;
+    constexpr double kOverlapLoss = 0.08, kMargin = 1.1;
+    constexpr double kBatchLatency = 1e-3;  // launch, H2D of a small batch, D2H, poll
+    const double threads = cpu_threads ? cpu_threads : 16;
+    const double rate = cpu_thread_rate > 0 ? cpu_thread_rate : 2.2e9;
+    const double L = piece_length, blocks = std::ceil((L + 9) / 64);
+    *out = vx_plan{};
+    if (n_pieces == 0) return 0;
+    const double chunk = 256.0 * 1024;
+    const double rounds = L >= 2 * chunk ? std::ceil(L / chunk) + 2 : 1;  // + the head/tail ramp rounds
+    out->gpu_chain_s = blocks * kChainBlock;
+    out->gpu_transfer_s = (double)total_length / kPcieRate;
+    const double pipe = out->gpu_chain_s + kSetup + rounds * kRound;
+    const double xfer = out->gpu_transfer_s + kSetup;
+    out->gpu_s = std::max(xfer, pipe) + kOverlapLoss * std::min(out->gpu_transfer_s, pipe);
+    out->cpu_s = std::ceil((double)n_pieces / threads) * (L / rate);
+    out->piece_latency_s = out->gpu_chain_s + kBatchLatency;
+    out->cpu_piece_latency_s = L / rate;
+    out->use_gpu = out->gpu_s * kMargin < out->cpu_s ? 1 : 0;
+    return 0;
 }
 
 uint64_t vx_tuning_chunk_rounds(const vx_ctx* c) { return c ? c->chunk_rounds : 0; }

@@ -251,6 +251,25 @@ def _verify_files(pool: "HashPool", paths: Sequence[str], file_lengths: Sequence
     return [bool(b) for b in out.raw[:count]], int(bad)
 
 
+def verify_files_multi(pools: Sequence["HashPool"], paths: Sequence[str], file_lengths: Sequence[int],
+                       piece_length: int, expected: bytes, io_threads: int = 0) -> tuple[list[bool], int]:
+    """In-process multi-GPU re-verify (vx_verify_files_multi): one HashPool
+    per GPU (or several on one), pieces split into contiguous ranges across
+    them, each range verified on its own host thread.  Same result as
+    HashPool.verify_files on one pool: (verdicts, pieces with I/O errors)."""
+    if not pools:
+        raise ValueError("need at least one pool")
+    n = len(expected) // 20
+    ctxs = (ctypes.c_void_p * len(pools))(*[p._h.value for p in pools])
+    arr = (ctypes.c_char_p * max(1, len(paths)))(*[os.fsencode(p) for p in paths])
+    lens = (ctypes.c_uint64 * max(1, len(file_lengths)))(*file_lengths)
+    exp = ctypes.create_string_buffer(bytes(expected), max(1, len(expected)))
+    out = ctypes.create_string_buffer(max(1, n))
+    rc = lib().vx_verify_files_multi(ctxs, len(pools), arr, lens, len(paths), piece_length, exp, n, out, io_threads)
+    bad = check(rc, "vx_verify_files_multi")
+    return [bool(b) for b in out.raw[:n]], int(bad)
+
+
 def _ptr_arrays(pieces: Sequence):
     n = len(pieces)
     keep = []
@@ -279,4 +298,4 @@ def piece_len(index: int, num_pieces: int, piece_length: int, total_length: int)
     return last if index == num_pieces - 1 else piece_length
 
 
-__all__ = ["DownloadedPiece", "HashPool", "verify_pieces", "piece_len"]
+__all__ = ["DownloadedPiece", "HashPool", "verify_pieces", "verify_files_multi", "piece_len"]
