@@ -72,3 +72,44 @@ def test_layout_all_gpu_paths(built, gpu, golden, tmp_path, name):
             assert sorted(res) == list(range(n))
             assert all(res[i][0] == (i != bad_piece) for i in range(n))
             assert all(res[i][1] == want[i] for i in range(n) if i != bad_piece)
+
+
+def test_fresh_fallocated_files(built, gpu, tmp_path):
+    """The re-verify vortex runs right after InitializedState::new, whose
+    FileStore::new creates every file and fallocates it to its torrent
+    length (file_store.rs:146, File::create at file_store.rs:22-43): regions
+    not downloaded yet read as zeros.  A piece whose real content is all
+    zeros therefore verifies true, pieces already written verify true, the
+    rest false, and no piece is an I/O error — the reference's verdicts
+    exactly (checked against the oracle's restatement too)."""
+    import oracle
+    from vortex_amd.hash_pool import HashPool
+
+    pl = 64 * 1024
+    sizes = [100_000, 3 * pl + 5, 17, 2 * pl]
+    data = bytearray(oracle.gen_piece(0xFA11, 0, sum(sizes)))
+    data[2 * pl:3 * pl] = bytes(pl)  # piece 2 really is all zeros
+    n = (len(data) + pl - 1) // pl
+    exp = b"".join(hashlib.sha1(bytes(data[i:i + pl])).digest() for i in range(0, len(data), pl))
+    paths, acc = [], 0
+    for k, L in enumerate(sizes):
+        p = tmp_path / f"f{k}"
+        with open(p, "wb") as f:
+            f.truncate(L)  # what fallocate leaves: L zero bytes
+        paths.append(str(p))
+    written = {0, 4}  # pieces the client already wrote (Write disk ops, file_store.rs:167-223)
+    for i in written:
+        lo, hi = i * pl, min((i + 1) * pl, len(data))
+        acc = 0
+        for p, L in zip(paths, sizes):
+            a, b = max(lo, acc), min(hi, acc + L)
+            if a < b:
+                with open(p, "r+b") as f:
+                    f.seek(a - acc)
+                    f.write(bytes(data[a:b]))
+            acc += L
+    want = [i in written or i == 2 for i in range(n)]
+    assert oracle.pool_verify_files(paths, sizes, pl, exp, threads=2) == want
+    with HashPool(pl) as pool:
+        got, nbad = pool.verify_files(paths, sizes, pl, exp)
+    assert got == want and nbad == 0

@@ -16,8 +16,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # Rust FFI scalar and handle types -> C base types
 RUST_TO_C = {
     "u8": "uint8_t", "u32": "uint32_t", "u64": "uint64_t", "i32": "int32_t", "i64": "int64_t",
-    "usize": "size_t", "c_int": "int", "c_char": "char", "c_void": "void",
-    "VxCtx": "vx_ctx", "VxConfig": "vx_config", "VxCompletion": "vx_completion",
+    "usize": "size_t", "c_int": "int", "c_char": "char", "c_void": "void", "f64": "double",
+    "VxCtx": "vx_ctx", "VxConfig": "vx_config", "VxCompletion": "vx_completion", "VxPlan": "vx_plan",
 }
 
 
@@ -140,7 +140,7 @@ def test_rust_externs_match_header():
 def test_rust_structs_match_header():
     c = c_structs()
     r = rust_structs()
-    pairs = {"VxCompletion": "vx_completion", "VxConfig": "vx_config"}
+    pairs = {"VxCompletion": "vx_completion", "VxConfig": "vx_config", "VxPlan": "vx_plan"}
     for rname, cname in pairs.items():
         assert r[rname] == c[cname], f"{rname} vs {cname}: {r[rname]} / {c[cname]}"
     assert r["VxCtx"] == [("_private", "uint8_t[0]")]  # opaque handle
