@@ -24,6 +24,7 @@
 #include <cstdlib>
 #include <stdint.h>
 
+#include "sha1_consumer_asm.inc"
 #include "sha1_device.hpp"
 #include "vx_kernels.h"
 
@@ -349,6 +350,35 @@ __device__ __forceinline__ void rounds_regs(State& s, const uint4 (&w)[20]) {
     s.h4 += e;
 }
 
+// Consumer for the 3-slot ring as ONE asm body (sha1_consumer_asm.inc,
+// generated and checked by tools/gen_sha1_rounds.py): hipcc's own schedule
+// and registers for the rounds ran a lone wave at ~4.5 cycles per VALU,
+// the fixed stream at ~4.06 including the ring reads
+// (tools/native/rounds_sched_probe.hip).  The asm holds the
+// block loop, the ring reads (block b+1's 20 ds_read_b128 in a burst at the
+// top of block b into the other of two word sets), the barriers (1 + nb_wave,
+// as the C++ consumer) and, with kSelect, the ragged phase-2 commit for
+// lanes with b < nb.  In the kernels it is 3-7 % faster per block than
+// hipcc's consumer (profiles/r02/consumer_asm/).  Build with
+// -DVX_CONSUMER_CC for the compiler-scheduled consumer (A/B).
+template <bool kSelect>
+__device__ __forceinline__ void consume_asm(State& s, const uint4* lds_lane, uint32_t nb_wave, uint32_t b1,
+                                            uint32_t nb) {
+    // LDS byte address: the low 32 bits of the generic address of a
+    // __shared__ object are its offset in the workgroup's LDS.
+    const uint32_t addr = (uint32_t)(uintptr_t)lds_lane;
+    if (kSelect)
+        asm volatile(VX_CONSUMER_SELECT_ASM
+                     : "+v"(s.h0), "+v"(s.h1), "+v"(s.h2), "+v"(s.h3), "+v"(s.h4)
+                     : "v"(addr), "s"(nb_wave), "s"(b1), "v"(nb)
+                     : VX_CONSUMER_SELECT_ASM_CLOBBERS, "memory");
+    else
+        asm volatile(VX_CONSUMER_ASM
+                     : "+v"(s.h0), "+v"(s.h1), "+v"(s.h2), "+v"(s.h3), "+v"(s.h4)
+                     : "v"(addr), "s"(nb_wave), "s"(b1), "v"(nb)
+                     : VX_CONSUMER_ASM_CLOBBERS, "memory");
+}
+
 // Consumer: compress blocks [0, nb_wave).  kSelect: blocks >= b1 commit only
 // for lanes with b < nb (ragged phase 2); otherwise b1 == nb_wave == nb.
 template <int S, bool kSelect>
@@ -370,6 +400,12 @@ __device__ __forceinline__ void consume(State& s, RingLds<S>& lds, int lane, uin
         }
         return;
     }
+#ifndef VX_CONSUMER_CC
+    if (S == 3) {
+        consume_asm<kSelect>(s, &lds.w[0][0][lane], nb_wave, b1, nb);
+        return;
+    }
+#endif
     if (nb_wave == 0) return;
     auto step = [&](uint32_t b, const uint4 (&r)[20]) {
         if (!kSelect || b < b1) {
