@@ -116,8 +116,12 @@ def consumer_regs(wbase: int) -> Regs:
                 f=["v79", "v80"], r="v81", k=["s20", "s21", "s22", "s23"])
 
 
-def _read(dst_base: int, q: int, slot: int) -> str:
-    return f"ds_read_b128 v[{dst_base + 4 * q}:{dst_base + 4 * q + 3}], %5 offset:{slot * SLOT_BYTES + q * QUAD_BYTES}"
+ADDR = "v87"  # burst2: LDS address of the next block's slot (base + s25)
+
+
+def _read(dst_base: int, q: int, slot: int, addr: str = "%5") -> str:
+    off = (slot * SLOT_BYTES if addr == "%5" else 0) + q * QUAD_BYTES
+    return f"ds_read_b128 v[{dst_base + 4 * q}:{dst_base + 4 * q + 3}], {addr} offset:{off}"
 
 
 def _block(R: Regs, mode: str, next_slot: int, next_base: int):
@@ -128,6 +132,8 @@ def _block(R: Regs, mode: str, next_slot: int, next_base: int):
     out = []
     if mode == "burst":
         out += [_read(next_base, q, next_slot) for q in range(20)]
+    elif mode == "burst2":
+        out += [f"v_add_u32_e64 {ADDR}, s25, %5"] + [_read(next_base, q, 0, ADDR) for q in range(20)]
     else:
         out += ["s_waitcnt lgkmcnt(15)", "s_nop 0"]
     out += body[0:3]  # prologue
@@ -143,7 +149,7 @@ def _block(R: Regs, mode: str, next_slot: int, next_base: int):
             out.append(_read(next_base, t, next_slot))
         out += chunk[1:]
     out += [f"v_add_u32_e64 {h}, {h}, {f}" for h, f in zip(R.h, final)]
-    if mode in ("burst", "spread"):
+    if mode in ("burst", "burst2", "spread"):
         out += ["s_waitcnt lgkmcnt(0)", "s_nop 0"]
     return out
 
@@ -165,16 +171,20 @@ def consumer_asm(select: bool, mode: str = "burst") -> str:
               consumer of the same form, while refill was 1.5-3.5 % slower
               and one read per round over rounds 0-19 5-9 % slower;
               profiles/r02/consumer_asm/);
+      burst2  as burst with a 2-block loop: the next slot's address is
+              base + s25 (one v_add and three SALU per block) instead of
+              immediate offsets, so the loop is a third of the code;
       spread  as burst, one read per round over rounds 0-19.
     Blocks b >= b1 (ragged phase 2, `select`) keep the new state only in
     lanes with b < nb (v_cndmask on v_cmp b < nb).  Hot-path instructions are
     8 bytes and scalar ones come in pairs, so bodies stay 8-byte aligned
     (DESIGN.md §3.6)."""
-    unroll = 3 if mode == "refill" else 6  # slots cycle by 3, word sets by 2
+    # slots cycle by 3, word sets by 2; burst2 addresses the slot through s25
+    unroll = {"refill": 3, "burst2": 2}.get(mode, 6)
     L = [f"v_mov_b32_e64 v{H0 + i}, %{i}" for i in range(5)]
     L += ["s_mov_b32 s20, 0x5a827999", "s_mov_b32 s21, 0x6ed9eba1", "s_mov_b32 s22, 0x8f1bbcdc",
-          "s_mov_b32 s23, 0xca62c1d6", "s_mov_b32 s24, 0", "s_cmp_eq_u32 %6, 0", "s_cbranch_scc1 .Lvx_end%=",
-          "s_barrier"]
+          "s_mov_b32 s23, 0xca62c1d6", "s_mov_b32 s24, 0", f"s_mov_b32 s25, {SLOT_BYTES}",
+          "s_cmp_eq_u32 %6, 0", "s_cbranch_scc1 .Lvx_end%=", "s_barrier"]
     L += [_read(WA, q, 0) for q in range(20)]
     L += ["s_waitcnt lgkmcnt(0)", "s_nop 0", ".p2align 5", ".Lvx_loop%=:"]
     for k in range(unroll):
@@ -192,17 +202,20 @@ def consumer_asm(select: bool, mode: str = "burst") -> str:
             L += [".p2align 3", f".Lvx_done{k}_%=:"]
         else:
             L += body
-        L += ["s_barrier", "s_add_u32 s24, s24, 1", "s_cmp_ge_u32 s24, %6", "s_cbranch_scc1 .Lvx_end%=",
-              ".p2align 3"]
+        L += ["s_barrier", "s_add_u32 s24, s24, 1"]
+        if mode == "burst2":  # next block's slot: (b + 2) % 3
+            L += [f"s_add_u32 s25, s25, {SLOT_BYTES}", f"s_cmp_eq_u32 s25, {3 * SLOT_BYTES}",
+                  "s_cselect_b32 s25, 0, s25", "s_nop 0"]
+        L += ["s_cmp_ge_u32 s24, %6", "s_cbranch_scc1 .Lvx_end%=", ".p2align 3"]
     L += ["s_branch .Lvx_loop%=", ".Lvx_end%=:", "s_waitcnt lgkmcnt(0)"]
     L += [f"v_mov_b32_e64 %{i}, v{H0 + i}" for i in range(5)]
     return "\n".join(L)
 
 
 def consumer_clobbers(select: bool, mode: str = "burst"):
-    v = [f"v{i}" for i in range(H0, SAVE0 + 5 if select else SAVE0)]
+    v = [f"v{i}" for i in range(H0, SAVE0 + 5 if select else SAVE0)] + ([ADDR] if mode == "burst2" else [])
     v += [f"v{i}" for i in range(WA, (WA if mode == "refill" else WB) + 80)]
-    return v + ["s20", "s21", "s22", "s23", "s24", "vcc"]
+    return v + ["s20", "s21", "s22", "s23", "s24", "s25", "vcc"]
 
 
 def write_consumer_header(path: str, mode: str) -> None:
@@ -304,7 +317,7 @@ def main():
     ap.add_argument("--emit", action="store_true", help="print the asm body (default registers)")
     ap.add_argument("--header", help="write a C header with the fixed-register block (probe use)")
     ap.add_argument("--consumer", help="write the split kernels' consumer asm header")
-    ap.add_argument("--mode", default="burst", choices=["refill", "burst", "spread"],
+    ap.add_argument("--mode", default="burst", choices=["refill", "burst", "burst2", "spread"],
                     help="ring-read placement (burst: the kernel's; A/B in DESIGN.md §3.2)")
     a = ap.parse_args()
     if a.check:

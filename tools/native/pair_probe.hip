@@ -1,0 +1,112 @@
+// pair_probe.hip — what costs the split kernel's consumer its last ~10 %?
+//
+// The generated consumer (vortex_amd/csrc/sha1_consumer_asm.inc) runs a block
+// in ~1,650 cycles alone (tools/native/rounds_sched_probe.hip) but ~1,850 in
+// the kernels.  This pairs it with a synthetic producer wave on the real
+// ring protocol (3 LDS slots, one barrier per block, RingLds layout) and
+// switches the producer's work on and off:
+//   0  producer passes the barriers only
+//   1  + writes each block's 20 x ds_write_b128 into its slot (as expand_store)
+//   2  + ~210 VALU per block (the schedule's load: 16 perm + 192 + stores' data)
+//   3  as 2, two pairs per CU (the kernels' occupancy with 60 KiB per pair)
+//   4  as 2 with the producer's VALU as a rolled loop (little instruction fetch)
+//   5  as 2 with the consumer at s_setprio 3
+// The consumer stamps s_memtime around its whole loop; prints cycles per
+// block (median over pairs) and the wall ns per block.  No HBM traffic.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <vector>
+
+#include "../../vortex_amd/csrc/sha1_consumer_asm.inc"
+
+struct Ring {
+    uint4 w[3][20][64];
+};
+
+template <int P>
+__global__ __launch_bounds__(128) void pair(uint32_t nb, uint32_t* out, unsigned long long* cyc) {
+    __shared__ Ring lds;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (wave == 1) {  // producer
+        uint32_t x = lane * 0x9E3779B9u, y = 0x12345u + lane;
+        for (uint32_t b = 0; b < nb; ++b) {
+            if (P == 4) {
+                // the same 210 VALU as a short rolled loop (no instruction-fetch stream)
+                for (int i = 0; i < 70; ++i) {
+                    x = __builtin_amdgcn_alignbit(x, x, 31) ^ y;
+                    y = __builtin_amdgcn_bitop3_b32(x, y, 0x5a5a5a5au, 0x96);
+                    x = x + y;
+                    asm volatile("" : "+v"(x), "+v"(y));
+                }
+            } else if (P >= 2) {
+#pragma unroll
+                for (int i = 0; i < 70; ++i) {  // 210 VALU
+                    x = __builtin_amdgcn_alignbit(x, x, 31) ^ y;
+                    y = __builtin_amdgcn_bitop3_b32(x, y, 0x5a5a5a5au, 0x96);
+                    x = x + y;
+                }
+            }
+            if (P >= 1) {
+#pragma unroll
+                for (int q = 0; q < 20; ++q) lds.w[b % 3][q][lane] = make_uint4(x + q, y, x ^ q, b);
+            }
+            if (b >= 1) __syncthreads();
+        }
+        if (nb) {
+            __syncthreads();
+            __syncthreads();
+        }
+        out[blockIdx.x * 64 + lane] = x ^ y;
+        return;
+    }
+    if (P == 5) __builtin_amdgcn_s_setprio(3);
+    uint32_t h0 = 0x67452301u + lane, h1 = 0xEFCDAB89u, h2 = 0x98BADCFEu, h3 = 0x10325476u, h4 = 0xC3D2E1F0u;
+    const uint32_t addr = (uint32_t)(uintptr_t)&lds.w[0][0][lane];
+    const uint32_t zero = 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    asm volatile(VX_CONSUMER_ASM
+                 : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3), "+v"(h4)
+                 : "v"(addr), "s"(nb), "s"(nb), "v"(zero)
+                 : VX_CONSUMER_ASM_CLOBBERS, "memory");
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    out[blockIdx.x * 64 + lane] = h0 ^ h1 ^ h2 ^ h3 ^ h4;
+    if (lane == 0) cyc[blockIdx.x] = t1 - t0;
+}
+
+template <int P>
+static void run(const char* name, int grid, uint32_t* d, unsigned long long* dc, bool comma) {
+    const uint32_t nb = 20000;
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    hipLaunchKernelGGL(pair<P>, dim3(grid), dim3(128), 0, 0, 500u, d, dc);
+    (void)hipEventRecord(a, 0);
+    hipLaunchKernelGGL(pair<P>, dim3(grid), dim3(128), 0, 0, nb, d, dc);
+    (void)hipEventRecord(b, 0);
+    (void)hipEventSynchronize(b);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, a, b);
+    std::vector<unsigned long long> c(grid);
+    (void)hipMemcpy(c.data(), dc, grid * 8, hipMemcpyDeviceToHost);
+    std::sort(c.begin(), c.end());
+    std::printf("%s\"%s\": {\"cycles_per_block\": %.1f, \"ns_per_block\": %.1f, \"pairs\": %d}", comma ? ", " : "",
+                name, (double)c[grid / 2] / nb, ms * 1e6 / nb, grid);
+}
+
+int main() {
+    uint32_t* d = nullptr;
+    unsigned long long* dc = nullptr;
+    if (hipMalloc(&d, 512 * 64 * 4) != hipSuccess || hipMalloc(&dc, 512 * 8) != hipSuccess) return 1;
+    std::printf("{");
+    run<0>("barriers_only", 64, d, dc, false);
+    run<1>("lds_writes", 64, d, dc, true);
+    run<2>("lds_writes_valu", 64, d, dc, true);
+    run<2>("lds_writes_valu_2_pairs_per_cu", 512, d, dc, true);
+    run<4>("lds_writes_valu_rolled_loop", 64, d, dc, true);
+    run<5>("lds_writes_valu_consumer_prio3", 64, d, dc, true);
+    std::printf("}\n");
+    return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
+}
