@@ -192,8 +192,8 @@ int64_t vx_verify_files_multi(vx_ctx* const* ctxs, size_t nctx, const char* cons
 
 /* ---- planning: where should a bulk verify run? (host-only, no GPU) -----
  * One piece is one lane on the GPU and SHA-1 cannot be split inside a
- * piece, so a few very long pieces are bound by one lane's chain (~0.81 us
- * per 64-byte block, ~79 MB/s), while vortex's own rayon + `sha1` pool
+ * piece, so a few very long pieces are bound by one lane's chain (~0.76 us
+ * per 64-byte block, ~84 MB/s), while vortex's own rayon + `sha1` pool
  * (torrent.rs:724-740) hashes one piece per core at ~2 GB/s.  This cost model
  * (calibrated on MI355X) predicts both for n_pieces pieces of
  * piece_length bytes (total_length in all, the last piece shorter) read from

@@ -223,8 +223,9 @@ def test_plan_verify_host(built):
 def test_plan_verify_matches_measured_grid(built):
     """The planner against the crossover grid measured on one MI355X
     (tools/crossover_grid.py -> profiles/r02/crossover/grid.json): the
-    decision equals the measured winner at every point, and the predicted
-    GPU time is within 20 % of the measured one."""
+    decision equals the measured winner wherever the two measured times
+    differ by more than 10 % (inside that the planner keeps the CPU pool by
+    design), and the predicted GPU time is within 10 % of the measured one."""
     import json
 
     with open(os.path.join(ROOT, "profiles", "r02", "crossover", "grid.json")) as f:
@@ -235,8 +236,11 @@ def test_plan_verify_matches_measured_grid(built):
         L = pt["piece_MiB"] * MiB
         rc, p = _plan(pt["n"], L, pt["n"] * L, threads=grid["threads"])
         assert rc == 0
-        assert p.use_gpu == (pt["winner"] == "gpu"), pt
-        assert abs(p.gpu_s / pt["gpu_s"] - 1) < 0.20, (pt, p.gpu_s)
+        if max(pt["gpu_s"], pt["cpu_s"]) > 1.1 * min(pt["gpu_s"], pt["cpu_s"]):
+            assert p.use_gpu == (pt["winner"] == "gpu"), pt
+        elif pt["winner"] == "cpu":
+            assert p.use_gpu == 0, pt
+        assert abs(p.gpu_s / pt["gpu_s"] - 1) < 0.10, (pt, p.gpu_s)
     for lp in grid["loop"]:  # download path: latency p50 ~ one piece's chain
         rc, p = _plan(1, lp["piece_len"], lp["piece_len"])
         assert abs(p.piece_latency_s * 1e3 / lp["latency_ms_p50"] - 1) < 0.15, lp

@@ -1772,22 +1772,23 @@ int vx_sha1_device_ragged_hint(const void* d_base, const uint64_t* d_offsets, co
 // Host-only cost model of a bulk verify.  One piece is one
 // lane and SHA-1 is Merkle-Damgård, so a piece of L bytes is a chain of
 // blocks(L) dependent compressions at kChainBlock seconds each on the split
-// kernel, and the chunk pipeline (§6.3) adds a fixed setup and a cost per
-// round of C = 256 KiB; the bytes cross PCIe at kPcieRate.  The call takes
-// the larger of the two, plus a fraction of the smaller (they overlap, but
-// not perfectly).  The caller's pool: ceil(n / threads) rounds of one piece
-// per thread at cpu_thread_rate bytes/s (rayon runs one piece per task,
-// torrent.rs:724-740).  Fitted to the measured grid of tools/crossover_grid.py
-// (profiles/r02/crossover/grid.json: 22 points, 2-16 MiB x 64-4,096 pieces,
-// GPU predictions within 8 % but one point at 17 %); tests/test_abi.py checks
-// the fit and every decision against that file.  use_gpu asks for a 10 %
-// margin: near a tie the caller's own pool is the safe choice.
+// kernels (the chunked re-verify pipelines its rounds, so the chain, not the
+// round count, is what remains); the bytes cross PCIe at kPcieRate.  The call
+// takes the larger of the two, a fixed setup, and a fraction of the smaller
+// (they overlap, but not perfectly).  The caller's pool: ceil(n / threads)
+// rounds of one piece per thread at cpu_thread_rate bytes/s (rayon runs one
+// piece per task, torrent.rs:724-740).  Fitted to the grid measured by
+// tools/crossover_grid.py on the asm-consumer build
+// (profiles/r02/crossover/grid.json: 22 points, 2-16 MiB x 64-4,096 pieces;
+// GPU predictions within 5 %); tests/test_abi.py checks the fit and every
+// decision against that file.  use_gpu asks for a 10 % margin: near a tie the
+// caller's own pool is the safe choice.
 int vx_plan_verify(uint64_t n_pieces, uint32_t piece_length, uint64_t total_length, uint32_t cpu_threads,
                    double cpu_thread_rate, vx_plan* out) {
     if (!out || piece_length == 0) return fail(VX_EINVAL, "vx_plan_verify: bad argument");
     if (n_pieces != (total_length + piece_length - 1) / piece_length)
         return fail(VX_EINVAL, "vx_plan_verify: n_pieces does not match total_length");
-    constexpr double kChainBlock = 0.81e-6, kPcieRate = 50.0 * (1ull << 30), kSetup = 3e-3, kRound = 0.6e-3;
+    constexpr double kChainBlock = 0.76e-6, kPcieRate = 52.0 * (1ull << 30), kSetup = 1.5e-3;
     constexpr double kOverlapLoss = 0.08, kMargin = 1.1;
     constexpr double kBatchLatency = 1e-3;  // launch, H2D of a small batch, D2H, poll
     const double threads = cpu_threads ? cpu_threads : 16;
@@ -1795,13 +1796,10 @@ int vx_plan_verify(uint64_t n_pieces, uint32_t piece_length, uint64_t total_leng
     const double L = piece_length, blocks = std::ceil((L + 9) / 64);
     *out = vx_plan{};
     if (n_pieces == 0) return 0;
-    const double chunk = 256.0 * 1024;
-    const double rounds = L >= 2 * chunk ? std::ceil(L / chunk) + 2 : 1;  // + the head/tail ramp rounds
     out->gpu_chain_s = blocks * kChainBlock;
     out->gpu_transfer_s = (double)total_length / kPcieRate;
-    const double pipe = out->gpu_chain_s + kSetup + rounds * kRound;
-    const double xfer = out->gpu_transfer_s + kSetup;
-    out->gpu_s = std::max(xfer, pipe) + kOverlapLoss * std::min(out->gpu_transfer_s, pipe);
+    out->gpu_s = std::max(out->gpu_transfer_s, out->gpu_chain_s) + kSetup +
+                 kOverlapLoss * std::min(out->gpu_transfer_s, out->gpu_chain_s);
     out->cpu_s = std::ceil((double)n_pieces / threads) * (L / rate);
     out->piece_latency_s = out->gpu_chain_s + kBatchLatency;
     out->cpu_piece_latency_s = L / rate;
