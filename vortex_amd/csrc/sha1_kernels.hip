@@ -850,9 +850,10 @@ namespace vx {
 // (DESIGN.md §3.4).  Each kernel's time is bounded below by its throughput
 // over all bytes and by the longest piece's chain, whichever is larger:
 //   lane : max(total / 3.4 TB/s, blocks(max_len) x 1.18 us)
-//   split: max(total / 2.5 TB/s, blocks(max_len) x 0.87 us)
+//   split: max(total / 2.5 TB/s, blocks(max_len) x 0.77 us)
 // (config 2 and config 3 measurements, §3.5: the lane kernel's VALU-bound
-// rate and per-block chain, the split kernel's).  Config 3's 4 MiB pieces make
+// rate and per-block chain, the split kernel's; 0.87 us before the asm
+// consumer of §3.2.1).  Config 3's 4 MiB pieces make
 // it chain-bound: 77 ms lane vs 57 ms split, though it has 283,648 pieces.
 //
 // Split batches whose whole-chip work at HALF the split throughput (one pair
@@ -861,9 +862,9 @@ int plan_ragged(uint32_t n, uint64_t max_len, uint64_t total_len) {
     (void)n;
     const double blocks = (double)((max_len + 9 + 63) / 64);
     const double lane = std::max((double)total_len / 3.4e12, blocks * 1.18e-6);
-    const double split = std::max((double)total_len / 2.5e12, blocks * 0.87e-6);
+    const double split = std::max((double)total_len / 2.5e12, blocks * 0.77e-6);
     if (lane < split) return kUniformLane;
-    return (double)total_len / 1.25e12 <= 0.5 * blocks * 0.87e-6 ? kSplitWide : kUniformSplit;
+    return (double)total_len / 1.25e12 <= 0.5 * blocks * 0.77e-6 ? kSplitWide : kUniformSplit;
 }
 
 // variant 0 without a plan: the split kernel.  A batch whose lengths really
