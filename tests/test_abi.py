@@ -85,6 +85,11 @@ def test_validation_without_gpu(built):
     bad = _lib.vx_config()
     assert L.vx_create(ctypes.byref(bad), ctypes.byref(h)) == _lib.VX_EINVAL
     assert L.vx_create(None, ctypes.byref(h)) == _lib.VX_EINVAL
+    # the multi-context re-verify validates its context list before any thread starts
+    assert L.vx_verify_files_multi(None, 2, None, None, 0, 256, None, 0, None, 0) == _lib.VX_EINVAL
+    ctxs = (ctypes.c_void_p * 2)(None, None)
+    assert L.vx_verify_files_multi(ctxs, 2, None, None, 0, 256, None, 0, None, 0) == _lib.VX_EINVAL
+    assert L.vx_verify_files_multi(ctxs, 0, None, None, 0, 256, None, 0, None, 0) == _lib.VX_EINVAL
 
 
 def test_sort_order_host_helper(built):
