@@ -120,7 +120,12 @@ ADDR = "v87"  # burst2: LDS address of the next block's slot (base + s25)
 
 
 def _read(dst_base: int, q: int, slot: int, addr: str = "%5") -> str:
-    off = (slot * SLOT_BYTES if addr == "%5" else 0) + q * QUAD_BYTES
+    """ds_read of quad q of ring slot `slot`.  Slots 0-2 are addressed from %5
+    (lds.w[0][0][lane]), slots 3-5 of the 6-slot ring from %9 (lds.w[3][0][lane])
+    so every offset fits the 16-bit field."""
+    if addr == "%5" and slot >= 3:
+        addr, slot = "%9", slot - 3
+    off = (slot * SLOT_BYTES if addr in ("%5", "%9") else 0) + q * QUAD_BYTES
     return f"ds_read_b128 v[{dst_base + 4 * q}:{dst_base + 4 * q + 3}], {addr} offset:{off}"
 
 
@@ -154,14 +159,18 @@ def _block(R: Regs, mode: str, next_slot: int, next_base: int):
     return out
 
 
-def consumer_asm(select: bool, mode: str = "burst") -> str:
-    """The whole consumer of sha1_*split_kernel (ring of 3 LDS slots) as one
-    asm body.  Operands: %0-%4 state h0-h4 ("+v"), %5 LDS byte address of
-    lds.w[0][0][lane] ("v"), %6 nb_wave ("s"), %7 b1 ("s"), %8 the lane's nb
-    ("v"; used only when `select`).
+def consumer_asm(select: bool, mode: str = "burst", slots: int = 3) -> str:
+    """The whole consumer of sha1_*split_kernel as one asm body.  Operands:
+    %0-%4 state h0-h4 ("+v"), %5 LDS byte address of lds.w[0][0][lane] ("v"),
+    %6 nb_wave ("s"), %7 b1 ("s"), %8 the lane's nb ("v"; used only when
+    `select`), and with slots = 6 %9 the address of lds.w[3][0][lane].
 
-    Barriers: none when nb_wave == 0, else one before block 0 and one after
-    every block (1 + nb_wave, matching the producer's publish/producer_done).
+    Barriers, slots = 3: none when nb_wave == 0, else one before block 0 and
+    one after every block (1 + nb_wave, matching the producer's publish /
+    producer_done).  slots = 6: one before block 0 and one after every PAIR of
+    blocks (the last pair may hold one block): 1 + ceil(nb_wave / 2); the
+    producer publishes pairs 0 and 1 before the first barrier and pair q + 1
+    before barrier q, and overwrites pair q's slots only after barrier q + 1.
     Ring reads of block b+1 (slot (b+1) % 3):
       refill  during block b, quad q right after its last use (X_{4q+3},
               round 4q+2), into the same registers: one word set; waits
@@ -179,8 +188,9 @@ def consumer_asm(select: bool, mode: str = "burst") -> str:
     lanes with b < nb (v_cndmask on v_cmp b < nb).  Hot-path instructions are
     8 bytes and scalar ones come in pairs, so bodies stay 8-byte aligned
     (DESIGN.md §3.6)."""
-    # slots cycle by 3, word sets by 2; burst2 addresses the slot through s25
+    # slots cycle by 3 (or 6), word sets by 2; burst2 addresses the slot through s25
     unroll = {"refill": 3, "burst2": 2}.get(mode, 6)
+    assert slots == 3 or (slots == 6 and mode == "burst")
     L = [f"v_mov_b32_e64 v{H0 + i}, %{i}" for i in range(5)]
     L += ["s_mov_b32 s20, 0x5a827999", "s_mov_b32 s21, 0x6ed9eba1", "s_mov_b32 s22, 0x8f1bbcdc",
           "s_mov_b32 s23, 0xca62c1d6", "s_mov_b32 s24, 0", f"s_mov_b32 s25, {SLOT_BYTES}",
@@ -190,7 +200,7 @@ def consumer_asm(select: bool, mode: str = "burst") -> str:
     for k in range(unroll):
         cur = WA if (mode == "refill" or k % 2 == 0) else WB
         nxt = WA if mode == "refill" else (WB if cur == WA else WA)
-        body = _block(consumer_regs(cur), mode, (k + 1) % 3, nxt)
+        body = _block(consumer_regs(cur), mode, (k + 1) % slots, nxt)
         if select:
             L += ["s_cmp_lt_u32 s24, %7", f"s_cbranch_scc0 .Lvx_sel{k}_%=", ".p2align 3"]
             L += body
@@ -202,6 +212,10 @@ def consumer_asm(select: bool, mode: str = "burst") -> str:
             L += [".p2align 3", f".Lvx_done{k}_%=:"]
         else:
             L += body
+        if slots == 6 and k % 2 == 0:  # first block of a pair: a barrier only if it is the last block
+            L += ["s_add_u32 s24, s24, 1", "s_cmp_ge_u32 s24, %6", f"s_cbranch_scc0 .Lvx_cont{k}_%=", "s_barrier",
+                  "s_branch .Lvx_end%=", "s_nop 0", ".p2align 3", f".Lvx_cont{k}_%=:"]
+            continue
         L += ["s_barrier", "s_add_u32 s24, s24, 1"]
         if mode == "burst2":  # next block's slot: (b + 2) % 3
             L += [f"s_add_u32 s25, s25, {SLOT_BYTES}", f"s_cmp_eq_u32 s25, {3 * SLOT_BYTES}",
@@ -225,9 +239,10 @@ def write_consumer_header(path: str, mode: str) -> None:
                 "// fixed issue order and registers for the 80 SHA-1 rounds (DESIGN.md §3.2).\n"
                 "// Checked by tests/test_rounds_gen.py (stream simulated against FIPS 180-4,\n"
                 f"// header up to date).  Ring reads: {mode}.\n#pragma once\n\n")
-        for name, sel in (("VX_CONSUMER_ASM", False), ("VX_CONSUMER_SELECT_ASM", True)):
+        for name, sel, slots in (("VX_CONSUMER_ASM", False, 3), ("VX_CONSUMER_SELECT_ASM", True, 3),
+                                 ("VX_CONSUMER6_ASM", False, 6), ("VX_CONSUMER6_SELECT_ASM", True, 6)):
             f.write(f"#define {name} \\\n")
-            for line in consumer_asm(sel, mode).splitlines():
+            for line in consumer_asm(sel, mode, slots).splitlines():
                 f.write(f'    "{line}\\n" \\\n')
             f.write('    ""\n')
             f.write(f"#define {name}_CLOBBERS " + ", ".join(f'"{r}"' for r in consumer_clobbers(sel, mode)) + "\n\n")

@@ -11,6 +11,7 @@
 //   3  as 2, two pairs per CU (the kernels' occupancy with 60 KiB per pair)
 //   4  as 2 with the producer's VALU as a rolled loop (little instruction fetch)
 //   5  as 2 with the consumer at s_setprio 3
+//   6  as 2 with a 6-slot ring and one barrier per PAIR of blocks (120 KiB LDS)
 // The consumer stamps s_memtime around its whole loop; prints cycles per
 // block (median over pairs) and the wall ns per block.  No HBM traffic.
 #include <hip/hip_runtime.h>
@@ -21,13 +22,15 @@
 
 #include "../../vortex_amd/csrc/sha1_consumer_asm.inc"
 
+template <int S>
 struct Ring {
-    uint4 w[3][20][64];
+    uint4 w[S][20][64];
 };
 
 template <int P>
 __global__ __launch_bounds__(128) void pair(uint32_t nb, uint32_t* out, unsigned long long* cyc) {
-    __shared__ Ring lds;
+    constexpr int S = P == 6 ? 6 : 3;  // 6: barrier per pair of blocks (VX_CONSUMER6_ASM)
+    __shared__ Ring<S> lds;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (wave == 1) {  // producer
@@ -51,9 +54,9 @@ __global__ __launch_bounds__(128) void pair(uint32_t nb, uint32_t* out, unsigned
             }
             if (P >= 1) {
 #pragma unroll
-                for (int q = 0; q < 20; ++q) lds.w[b % 3][q][lane] = make_uint4(x + q, y, x ^ q, b);
+                for (int q = 0; q < 20; ++q) lds.w[b % S][q][lane] = make_uint4(x + q, y, x ^ q, b);
             }
-            if (b >= 1) __syncthreads();
+            if (S == 3 ? b >= 1 : ((b & 1) || b + 1 == nb) && b >= 2) __syncthreads();
         }
         if (nb) {
             __syncthreads();
@@ -65,12 +68,19 @@ __global__ __launch_bounds__(128) void pair(uint32_t nb, uint32_t* out, unsigned
     if (P == 5) __builtin_amdgcn_s_setprio(3);
     uint32_t h0 = 0x67452301u + lane, h1 = 0xEFCDAB89u, h2 = 0x98BADCFEu, h3 = 0x10325476u, h4 = 0xC3D2E1F0u;
     const uint32_t addr = (uint32_t)(uintptr_t)&lds.w[0][0][lane];
+    const uint32_t addr3 = (uint32_t)(uintptr_t)&lds.w[S == 6 ? 3 : 0][0][lane];
     const uint32_t zero = 0;
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    asm volatile(VX_CONSUMER_ASM
-                 : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3), "+v"(h4)
-                 : "v"(addr), "s"(nb), "s"(nb), "v"(zero)
-                 : VX_CONSUMER_ASM_CLOBBERS, "memory");
+    if (S == 6)
+        asm volatile(VX_CONSUMER6_ASM
+                     : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3), "+v"(h4)
+                     : "v"(addr), "s"(nb), "s"(nb), "v"(zero), "v"(addr3)
+                     : VX_CONSUMER6_ASM_CLOBBERS, "memory");
+    else
+        asm volatile(VX_CONSUMER_ASM
+                     : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3), "+v"(h4)
+                     : "v"(addr), "s"(nb), "s"(nb), "v"(zero)
+                     : VX_CONSUMER_ASM_CLOBBERS, "memory");
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     out[blockIdx.x * 64 + lane] = h0 ^ h1 ^ h2 ^ h3 ^ h4;
     if (lane == 0) cyc[blockIdx.x] = t1 - t0;
@@ -107,6 +117,7 @@ int main() {
     run<2>("lds_writes_valu_2_pairs_per_cu", 512, d, dc, true);
     run<4>("lds_writes_valu_rolled_loop", 64, d, dc, true);
     run<5>("lds_writes_valu_consumer_prio3", 64, d, dc, true);
+    run<6>("lds_writes_valu_6slots_barrier_per_pair", 64, d, dc, true);
     std::printf("}\n");
     return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
