@@ -7,8 +7,7 @@
  *   feeds a rounds-only wave through an LDS ring), 3 / 4 = split with a 2- / 3-slot
  *   LDS ring (A/B of the ring protocol; 2 uses the default ring), 5 = split
  *   with one pair per CU (ragged only; what the planner picks for batches
- *   bound by their longest chain), 6 = split with a 6-slot ring and one
- *   barrier per pair of blocks (120 KiB per pair: one pair per CU; A/B).
+ *   bound by their longest chain).
  */
 #ifndef VX_TUNING_H
 #define VX_TUNING_H

@@ -40,7 +40,7 @@ def _ragged_upload(torch, dev, pieces, align=16):
                                                                                dtype=torch.int32, device=dev)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 6])
+@pytest.mark.parametrize("variant", [1, 2])
 def test_uniform_lengths_vs_oracle(built, gpu, variant):
     import torch
 
@@ -357,7 +357,7 @@ def test_idempotent_and_stream_ordering(built, gpu):
     assert a.cpu().numpy().tobytes() == oracle.pool_digest_synth(1, 0, n, plen, threads=THREADS)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 5, 6])
+@pytest.mark.parametrize("variant", [1, 2, 5])
 def test_ragged_variants_vs_oracle(built, gpu, variant):
     """Both ragged kernels on a mixed batch (0..4 MiB, odd lengths), lane order
     sorted and unsorted, with verdicts."""

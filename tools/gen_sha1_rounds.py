@@ -232,15 +232,16 @@ def consumer_clobbers(select: bool, mode: str = "burst"):
     return v + ["s20", "s21", "s22", "s23", "s24", "s25", "vcc"]
 
 
-def write_consumer_header(path: str, mode: str) -> None:
+def write_consumer_header(path: str, mode: str, slots: int = 3) -> None:
     with open(path, "w") as f:
         f.write("// GENERATED by tools/gen_sha1_rounds.py --consumer; do not edit.\n"
                 "// The split kernels' consumer loop (ring of 3 LDS slots) as one asm body:\n"
                 "// fixed issue order and registers for the 80 SHA-1 rounds (DESIGN.md §3.2).\n"
                 "// Checked by tests/test_rounds_gen.py (stream simulated against FIPS 180-4,\n"
                 f"// header up to date).  Ring reads: {mode}.\n#pragma once\n\n")
-        for name, sel, slots in (("VX_CONSUMER_ASM", False, 3), ("VX_CONSUMER_SELECT_ASM", True, 3),
-                                 ("VX_CONSUMER6_ASM", False, 6), ("VX_CONSUMER6_SELECT_ASM", True, 6)):
+        names = (("VX_CONSUMER_ASM", False), ("VX_CONSUMER_SELECT_ASM", True)) if slots == 3 else \
+            (("VX_CONSUMER6_ASM", False), ("VX_CONSUMER6_SELECT_ASM", True))
+        for name, sel in names:
             f.write(f"#define {name} \\\n")
             for line in consumer_asm(sel, mode, slots).splitlines():
                 f.write(f'    "{line}\\n" \\\n')
@@ -332,6 +333,8 @@ def main():
     ap.add_argument("--emit", action="store_true", help="print the asm body (default registers)")
     ap.add_argument("--header", help="write a C header with the fixed-register block (probe use)")
     ap.add_argument("--consumer", help="write the split kernels' consumer asm header")
+    ap.add_argument("--consumer6", help="write the 6-slot, barrier-per-pair consumer header (probe only: "
+                                           "no faster in the kernels, DESIGN.md §3.2.1)")
     ap.add_argument("--mode", default="burst", choices=["refill", "burst", "burst2", "spread"],
                     help="ring-read placement (burst: the kernel's; A/B in DESIGN.md §3.2)")
     a = ap.parse_args()
@@ -343,6 +346,8 @@ def main():
         print(emit(ins, final, R.h))
     if a.consumer:
         write_consumer_header(a.consumer, a.mode)
+    if a.consumer6:
+        write_consumer_header(a.consumer6, a.mode, slots=6)
     if a.header:
         body = emit(ins, final, R.h)
         regs = sorted({r for r in R.h + R.w + R.a + R.c + R.x + R.f + [R.r]}, key=lambda r: int(r[1:]))

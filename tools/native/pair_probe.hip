@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "../../vortex_amd/csrc/sha1_consumer_asm.inc"
+#include "sha1_consumer6_asm.inc"  // python tools/gen_sha1_rounds.py --consumer6 tools/native/sha1_consumer6_asm.inc
 
 template <int S>
 struct Ring {

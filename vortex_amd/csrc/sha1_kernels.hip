@@ -289,19 +289,12 @@ struct RingLds {
 
 template <int S>
 __device__ __forceinline__ uint32_t ring_slot(uint32_t b) {
-    return S == 2 ? (b & 1u) : (b % (uint32_t)S);
+    return S == 2 ? (b & 1u) : (b % 3u);
 }
 
-// Producer: block b (of nb_wave) is in its slot.  S = 3 publishes blocks 0
-// and 1 together, then one block per barrier.  S = 6 (one barrier per PAIR of
-// blocks, VX_CONSUMER6_ASM): pairs 0 and 1 together, then one pair per
-// barrier; a pair ends at an odd block or at the last block.
+// Producer: block b is in its slot.  S = 3 publishes blocks 0 and 1 together.
 template <int S>
-__device__ __forceinline__ void publish(uint32_t b, uint32_t nb_wave) {
-    if (S == 6) {
-        if (b >= 2 && ((b & 1u) || b + 1 == nb_wave)) __syncthreads();
-        return;
-    }
+__device__ __forceinline__ void publish(uint32_t b) {
     if (S == 2 || b >= 1) __syncthreads();
 }
 
@@ -386,26 +379,6 @@ __device__ __forceinline__ void consume_asm(State& s, const uint4* lds_lane, uin
                      : VX_CONSUMER_ASM_CLOBBERS, "memory");
 }
 
-// The 6-slot ring (120 KiB per pair: one pair per CU), one barrier per pair of
-// blocks instead of per block (VX_CONSUMER6_ASM; slots 3-5 addressed from a
-// second base so every ds_read offset fits 16 bits).
-template <bool kSelect>
-__device__ __forceinline__ void consume_asm6(State& s, const uint4* lds_lane, const uint4* lds_lane3,
-                                             uint32_t nb_wave, uint32_t b1, uint32_t nb) {
-    const uint32_t addr = (uint32_t)(uintptr_t)lds_lane;
-    const uint32_t addr3 = (uint32_t)(uintptr_t)lds_lane3;
-    if (kSelect)
-        asm volatile(VX_CONSUMER6_SELECT_ASM
-                     : "+v"(s.h0), "+v"(s.h1), "+v"(s.h2), "+v"(s.h3), "+v"(s.h4)
-                     : "v"(addr), "s"(nb_wave), "s"(b1), "v"(nb), "v"(addr3)
-                     : VX_CONSUMER6_SELECT_ASM_CLOBBERS, "memory");
-    else
-        asm volatile(VX_CONSUMER6_ASM
-                     : "+v"(s.h0), "+v"(s.h1), "+v"(s.h2), "+v"(s.h3), "+v"(s.h4)
-                     : "v"(addr), "s"(nb_wave), "s"(b1), "v"(nb), "v"(addr3)
-                     : VX_CONSUMER6_ASM_CLOBBERS, "memory");
-}
-
 // Consumer: compress blocks [0, nb_wave).  kSelect: blocks >= b1 commit only
 // for lanes with b < nb (ragged phase 2); otherwise b1 == nb_wave == nb.
 template <int S, bool kSelect>
@@ -425,10 +398,6 @@ __device__ __forceinline__ void consume(State& s, RingLds<S>& lds, int lane, uin
                 __syncthreads();
             }
         }
-        return;
-    }
-    if (S == 6) {
-        consume_asm6<kSelect>(s, &lds.w[0][0][lane], &lds.w[S == 6 ? 3 : 0][0][lane], nb_wave, b1, nb);
         return;
     }
 #ifndef VX_CONSUMER_CC
@@ -552,11 +521,11 @@ __global__ __launch_bounds__(kPairBlock) void sha1_split_kernel(const uint8_t* _
                     if (g0 + r < ng) {
                         le_words(w, ring[r][0], ring[r][1], ring[r][2], ring[r][3]);
                         expand_store(w, lds.w[ring_slot<S>(b)], lane);
-                        publish<S>(b, nb);
+                        publish<S>(b);
                         ++b;
                         le_words(w, ring[r][4], ring[r][5], ring[r][6], ring[r][7]);
                         expand_store(w, lds.w[ring_slot<S>(b)], lane);
-                        publish<S>(b, nb);
+                        publish<S>(b);
                         ++b;
                     }
                 }
@@ -567,7 +536,7 @@ __global__ __launch_bounds__(kPairBlock) void sha1_split_kernel(const uint8_t* _
             const uint4* q4 = reinterpret_cast<const uint4*>(q);
             le_words(w, q4[0], q4[1], q4[2], q4[3]);
             expand_store(w, lds.w[ring_slot<S>(b)], lane);
-            publish<S>(b, nb);
+            publish<S>(b);
             ++b;
             q += 64;
         }
@@ -578,17 +547,17 @@ __global__ __launch_bounds__(kPairBlock) void sha1_split_kernel(const uint8_t* _
             w[14] = bits_hi;
             w[15] = bits_lo;
             expand_store(w, lds.w[ring_slot<S>(b)], lane);
-            publish<S>(b, nb);
+            publish<S>(b);
         } else {
             expand_store(w, lds.w[ring_slot<S>(b)], lane);
-            publish<S>(b, nb);
+            publish<S>(b);
             ++b;
 #pragma unroll
             for (int k = 0; k < 14; ++k) w[k] = 0;
             w[14] = bits_hi;
             w[15] = bits_lo;
             expand_store(w, lds.w[ring_slot<S>(b)], lane);
-            publish<S>(b, nb);
+            publish<S>(b);
         }
         producer_done<S>(nb);
     } else {
@@ -714,7 +683,7 @@ __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
                     __builtin_amdgcn_sched_barrier(0);
                     le_words(w, ring[r][0], ring[r][1], ring[r][2], ring[r][3]);
                     expand_store(w, lds.w[ring_slot<S>(b0 + r)], lane);
-                    publish<S>(b0 + r, nb_wave);
+                    publish<S>(b0 + r);
                 }
             }
         }
@@ -760,7 +729,7 @@ __global__ __launch_bounds__(kPairBlock) void sha1_ragged_split_kernel(
                             w[k] = v;
                         }
                         expand_store(w, lds.w[ring_slot<S>(b)], lane);
-                        publish<S>(b, nb_wave);
+                        publish<S>(b);
                     }
                 }
             }
@@ -866,8 +835,6 @@ hipError_t launch_uniform(const uint8_t* base, uint64_t stride, uint32_t len, ui
         return launch_uniform_split_s<2>(base, stride, len, n, digests, expected, matched, stream, exp_index);
     if (variant == kSplitRing3)
         return launch_uniform_split_s<3>(base, stride, len, n, digests, expected, matched, stream, exp_index);
-    if (variant == kSplitPair)
-        return launch_uniform_split_s<6>(base, stride, len, n, digests, expected, matched, stream, exp_index);
     // Default: the integer VALU is the roofline once every SIMD has a wave
     // (n >= 65,536 with the lane kernel), and the split kernel's extra LDS
     // hand-off only costs there.  Below kSplitMaxPieces the chip has idle
@@ -916,8 +883,6 @@ hipError_t launch_ragged(const uint8_t* base, const uint64_t* offsets, const uin
     if (variant == kSplitWide)
         return launch_ragged_split_s<kSplitSlots>(base, offsets, lens, order, n, digests, expected, matched, stream,
                                                   exp_index, true);
-    if (variant == kSplitPair)
-        return launch_ragged_split_s<6>(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
     return launch_ragged_split(base, offsets, lens, order, n, digests, expected, matched, stream, exp_index);
 }
 }  // namespace vx

@@ -1723,7 +1723,7 @@ int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t
     if ((reinterpret_cast<uintptr_t>(d_base) & 15) || (stride & 15))
         return fail(VX_EINVAL, "vx_sha1_device_uniform: base and stride must be 16-byte aligned");
     if (n > 1 && stride < len) return fail(VX_EINVAL, "vx_sha1_device_uniform: stride < len");
-    if (variant < 0 || variant > vx::kSplitPair || variant == vx::kSplitWide)
+    if (variant < 0 || variant > 4)
         return fail(VX_EINVAL, "vx_sha1_device_uniform: unknown variant");
     hipError_t e = vx::launch_uniform(static_cast<const uint8_t*>(d_base), stride, len, n,
                                       static_cast<uint8_t*>(d_digests), static_cast<const uint8_t*>(d_expected),
@@ -1747,7 +1747,7 @@ int vx_sha1_device_ragged_variant(const void* d_base, const uint64_t* d_offsets,
     if (d_matched && !d_expected) return fail(VX_EINVAL, "vx_sha1_device_ragged: d_matched needs d_expected");
     if (reinterpret_cast<uintptr_t>(d_base) & 15)
         return fail(VX_EINVAL, "vx_sha1_device_ragged: base must be 16-byte aligned");
-    if (variant < 0 || variant > vx::kSplitPair) return fail(VX_EINVAL, "vx_sha1_device_ragged: unknown variant");
+    if (variant < 0 || variant > vx::kSplitWide) return fail(VX_EINVAL, "vx_sha1_device_ragged: unknown variant");
     hipError_t e = vx::launch_ragged(static_cast<const uint8_t*>(d_base), d_offsets, d_lens, d_order, n,
                                      static_cast<uint8_t*>(d_digests), static_cast<const uint8_t*>(d_expected),
                                      static_cast<uint8_t*>(d_matched), static_cast<hipStream_t>(stream), variant);

@@ -21,8 +21,7 @@ enum UniformVariant {
     kUniformSplit = 2,
     kSplitRing2 = 3,
     kSplitRing3 = 4,
-    kSplitWide = 5,
-    kSplitPair = 6  // 6-slot ring, one barrier per pair of blocks, one pair per CU (A/B)
+    kSplitWide = 5
 };
 // LDS ring slots of the split kernels (sha1_kernels.hip "Ring protocol").
 // 3: the producer runs two blocks ahead and the consumer prefetches the next
