@@ -155,6 +155,7 @@ struct vx_ctx {
     int verify_ramp = 1;  // ramp depth d: first/last rounds C / 2^(d+1) (0 = off)
     uint64_t verify_chunked_above = 0;
     bool verify_overlap = true;  // read round k+1 while round k is enqueued (VX_VERIFY_OVERLAP)
+    uint32_t verify_readahead = 2;  // chunked re-verify: rounds read ahead of the enqueue (VX_VERIFY_READAHEAD)
     uint64_t chunk_rounds = 0;  // chunk rounds launched (vx_tuning_chunk_rounds)
     // Per-piece device rows of the chunk paths (state | expected | digest |
     // verdict), kept across calls and grown on demand: allocating them per
@@ -725,6 +726,7 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (const char* m = std::getenv("VX_VERIFY_RAMP")) c->verify_ramp = std::max(0, std::min(5, std::atoi(m)));
     if (const char* m = std::getenv("VX_VERIFY_CHUNKED_ABOVE")) c->verify_chunked_above = std::strtoull(m, nullptr, 0);
     if (const char* m = std::getenv("VX_VERIFY_OVERLAP")) c->verify_overlap = std::atoi(m) != 0;
+    if (const char* m = std::getenv("VX_VERIFY_READAHEAD")) c->verify_readahead = (uint32_t)std::max(1, std::atoi(m));
     int rc = set_device(c);
     if (!rc && c->h2d_mode == 3 && hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess)
         rc = fail(VX_EDEVICE, "vx_create: copy stream");
@@ -1055,32 +1057,58 @@ struct ChunkPipe {
     template <class F>
     int free_slot(F&& on_reap) {
         for (;;) {
-            for (int k = 0; k < (int)c->slots.size(); ++k)
+            bool inflight = false;
+            for (int k = 0; k < (int)c->slots.size(); ++k) {
                 if (c->slots[k].state == Slot::FREE) return k;
+                inflight |= c->slots[k].state == Slot::INFLIGHT;
+            }
+            if (!inflight) return fail(VX_EDEVICE, "chunk rounds: no slot to wait for");
             int rc = reap(c, true);
             on_reap();
             if (rc) return rc;
         }
     }
+    // A slot that is free now, after polling completions without blocking;
+    // -1 in *si when there is none.
+    template <class F>
+    int try_free_slot(int* si, F&& on_reap) {
+        *si = -1;
+        const int rc = reap(c, false);
+        on_reap();
+        if (rc) return rc;
+        for (int k = 0; k < (int)c->slots.size(); ++k)
+            if (c->slots[k].state == Slot::FREE) {
+                *si = k;
+                break;
+            }
+        return 0;
+    }
 
     // Slot si's h_offsets/h_lens/h_pidx/h_poff/h_tlen [0, m) describe the
-    // round's lanes; they go to the device first, then copy_data(slot,
-    // stream) enqueues the chunk bytes into the slot arena (a copy, or the
-    // gather kernel, which reads d_offsets/d_lens).  continues = the round
-    // follows one of the same window.
+    // round's lanes; copy_data(slot, stream) enqueues the chunk bytes into the
+    // slot arena.  The lane table goes up as ONE copy of the metadata block's
+    // head (offsets | chunk offsets | total lens | gather sources | lens |
+    // piece rows, alloc_slot), not five: each small H2D is a blit kernel, and
+    // five of them put ~0.1 ms between one round's data copy and the next.
+    // When copy_data is a plain copy the table follows it, after `copied`, so
+    // the next round's data copy (chained on `copied`) need not wait for it;
+    // a gather (meta_first) reads d_offsets/d_lens, so the table goes first.
+    // continues = the round follows one of the same window.
     template <class F>
-    int round(int si, uint32_t m, bool continues, F&& copy_data) {
+    int round(int si, uint32_t m, bool continues, bool meta_first, F&& copy_data) {
         Slot& s = c->slots[si];
         hipStream_t st = s.stream;
         int rc = chain_h2d(c, si);
-        if (!rc && (hipMemcpyAsync(s.d_offsets, s.h_offsets, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
-                    hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)m * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
-                    hipMemcpyAsync(s.d_pidx, s.h_pidx, (size_t)m * 4, hipMemcpyHostToDevice, st) != hipSuccess ||
-                    hipMemcpyAsync(s.d_poff, s.h_poff, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
-                    hipMemcpyAsync(s.d_tlen, s.h_tlen, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess))
-            rc = fail(VX_EDEVICE, "chunk round: H2D failed");
+        const size_t meta = (size_t)(reinterpret_cast<const uint8_t*>(s.h_pidx + m) - reinterpret_cast<const uint8_t*>(s.h_offsets));
+        auto table = [&] {
+            if (hipMemcpyAsync(s.d_offsets, s.h_offsets, meta, hipMemcpyHostToDevice, st) != hipSuccess)
+                return fail(VX_EDEVICE, "chunk round: H2D failed");
+            return 0;
+        };
+        if (!rc && meta_first) rc = table();
         if (!rc) rc = copy_data(s, st);
         if (!rc && hipEventRecord(s.copied, st) != hipSuccess) rc = fail(VX_EDEVICE, "chunk round: event failed");
+        if (!rc && !meta_first) rc = table();
         mark_launched(c, si);
         if (!rc && continues && have_prev && hipStreamWaitEvent(st, prev_kernel, 0) != hipSuccess)
             rc = fail(VX_EDEVICE, "chunk round: stream wait failed");
@@ -1163,11 +1191,15 @@ std::vector<std::pair<uint64_t, uint64_t>> chunk_schedule(uint64_t L, uint64_t C
     return r;
 }
 
-// Round k+1 is read while round k is enqueued: the enqueue (chain_h2d waits
-// for the copy two rounds back, then metadata copies and the launch) took
-// 0.8-0.9 ms of host time per 256 KiB round, and with the read (5.5 ms) in
-// series the host needed 6.4 ms per round against a 6.35 ms H2D, so the copy
-// engine idled between rounds (VX_TRACE_ROUNDS).
+// The rounds of every window, in order, each read into its own slot by the
+// reader pool and then enqueued (H2D + chunk kernel).  Reads run up to
+// `verify_readahead` rounds ahead of the round being enqueued (bounded by the
+// slots), queued on the pool so the readers never wait for an enqueue: with
+// one round of read-ahead the reads and the copy chain were coupled round by
+// round, and every round whose read outlasted the previous copy left PCIe
+// idle (the head ramp's doubling rounds most of all).
+// VX_TRACE_ROUNDS=1 prints per-round host timings and, after the call, each
+// round's data copy as the GPU timed it.
 int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl, uint64_t total, uint64_t first,
                    uint64_t end, uint64_t C) {
     vx_ctx* c = fv.c;
@@ -1175,11 +1207,28 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     const uint64_t cnt = end - first;
     ChunkPipe cp(c);
     int rc = cp.open(cnt, fv.expected + 20 * first, "vx_verify_files");
-    std::vector<vx_files::ReadItem> items[2];  // round k+1 reads while round k's are still referenced
     // windows of W pieces; each window runs its rounds in order
     const Slot& s0 = c->slots[0];
     const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>(s0.cap, s0.arena_cap / C));
-    // VX_TRACE_ROUNDS=1: per-round host timings on stderr
+    struct Round {
+        uint64_t w0, w1, a, len;
+        bool continues;
+        int si;
+        uint32_t m;
+        uint64_t ticket, bytes;
+    };
+    std::vector<Round> rounds;
+    for (uint64_t w0 = first; w0 < end; w0 += W) {
+        const uint64_t w1 = std::min<uint64_t>(end, w0 + W);
+        const uint64_t wmax = w1 == n ? std::max<uint64_t>(pl, last_len) : pl;
+        const auto sched = chunk_schedule(wmax, C, w0 == first ? c->verify_ramp : 0, w1 == end ? c->verify_ramp : 0);
+        for (size_t k = 0; k < sched.size(); ++k)
+            rounds.push_back(Round{w0, w1, sched[k].first, sched[k].second, k > 0, -1, 0, 0, 0});
+    }
+    const size_t nslots = c->slots.size();
+    const size_t depth =
+        c->verify_overlap && nslots > 1 ? std::min<size_t>(std::max<uint32_t>(1, c->verify_readahead), nslots - 1) : 0;
+    std::vector<std::vector<vx_files::ReadItem>> items(nslots);
     static const bool trace = [] {
         const char* e = std::getenv("VX_TRACE_ROUNDS");
         return e && e[0] == '1';
@@ -1189,84 +1238,96 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     auto ms = [](clk::time_point a, clk::time_point b) {
         return std::chrono::duration<double, std::milli>(b - a).count();
     };
-    struct Pending {
+    std::vector<hipEvent_t> tev;  // trace: a (start, end) pair per round's data copy
+    auto consume = [&] { fv.consume(); };
+    // Reserve a slot for round r and queue its reads; false when no slot is
+    // free and `block` is not set.
+    auto start_read = [&](Round& r, bool block) -> bool {
         int si = -1;
+        if (block) {
+            si = cp.free_slot(consume);
+            if (si < 0) rc = si;
+        } else {
+            rc = cp.try_free_slot(&si, consume);
+        }
+        if (rc || si < 0) return false;
+        Slot& s = c->slots[si];
+        reset_fill(s);
+        if ((rc = ensure_stage(s))) return false;
+        const uint64_t pitch = align_up(r.len, kAlign);
+        auto& it = items[si];
+        it.clear();
         uint32_t m = 0;
-        bool continues = false;
-    } prev;
-    auto enqueue = [&]() -> int {
-        if (prev.si < 0) return 0;
-        const auto t0 = clk::now();
-        const int r = cp.round(prev.si, prev.m, prev.continues, [&](Slot& sl, hipStream_t st) {
+        for (uint64_t i = r.w0; i < r.w1; ++i) {
+            const uint64_t len_i = i == n - 1 ? last_len : pl;
+            if (r.a >= len_i && !(r.a == 0 && len_i == 0)) continue;  // piece already finished
+            const uint64_t clen = std::min<uint64_t>(r.len, len_i - r.a);
+            it.push_back(vx_files::ReadItem{s.h_stage + (uint64_t)m * pitch, i, r.a, clen});
+            s.h_offsets[m] = (uint64_t)m * pitch;
+            s.h_lens[m] = (uint32_t)clen;
+            s.h_pidx[m] = (uint32_t)(i - first);
+            s.h_poff[m] = r.a;
+            s.h_tlen[m] = len_i;
+            ++m;
+        }
+        r.m = m;
+        if (m == 0) return true;  // nothing to read or hash: the slot stays free
+        s.state = Slot::FILLING;  // reserved until the round is enqueued
+        s.bytes = r.bytes = (uint64_t)(m - 1) * pitch + s.h_lens[m - 1];
+        r.si = si;
+        r.ticket = rd.submit(it);
+        return true;
+    };
+    size_t nr = 0;  // next round to read
+    for (size_t ne = 0; ne < rounds.size() && !rc; ++ne) {
+        const auto t_a = clk::now();
+        while (nr < rounds.size() && nr <= ne + depth && start_read(rounds[nr], nr == ne)) ++nr;
+        if (rc) break;
+        Round& r = rounds[ne];
+        if (r.m == 0) continue;
+        const auto t_b = clk::now();
+        rd.wait(r.ticket);
+        const auto t_c = clk::now();
+        rc = cp.round(r.si, r.m, r.continues, false, [&](Slot& sl, hipStream_t st) {
+            if (trace) {
+                tev.resize(tev.size() + 2, nullptr);
+                (void)hipEventCreate(&tev[tev.size() - 2]);
+                (void)hipEventCreate(&tev[tev.size() - 1]);
+                (void)hipEventRecord(tev[tev.size() - 2], st);
+            }
             if (hipMemcpyAsync(sl.d_arena, sl.h_stage, sl.bytes, hipMemcpyHostToDevice, st) != hipSuccess)
                 return fail(VX_EDEVICE, "vx_verify_files: chunk H2D failed");
+            if (trace) (void)hipEventRecord(tev.back(), st);
             return 0;
         });
-        if (trace) std::fprintf(stderr, "vx   enqueue slot %d: %.2f ms\n", prev.si, ms(t0, clk::now()));
-        prev.si = -1;
-        return r;
-    };
-    int buf = 0;
-    for (uint64_t w0 = first; w0 < end && !rc; w0 += W) {
-        const uint64_t w1 = std::min<uint64_t>(end, w0 + W);
-        const uint64_t wmax = w1 == n ? std::max<uint64_t>(pl, last_len) : pl;
-        const auto sched =
-            chunk_schedule(wmax, C, w0 == first ? c->verify_ramp : 0, w1 == end ? c->verify_ramp : 0);
-        for (size_t k = 0; k < sched.size() && !rc; ++k) {
-            const uint64_t a = sched[k].first, rlen = sched[k].second;
-            const uint64_t pitch = align_up(rlen, kAlign);
-            if ((c->slots.size() < 2 || !c->verify_overlap) && (rc = enqueue())) break;  // one slot: nothing to overlap with
-            const auto t_a = clk::now();
-            const int si = cp.free_slot([&] { fv.consume(); });
-            const auto t_b = clk::now();
-            if (si < 0) {
-                rc = si;
-                break;
-            }
-            Slot& s = c->slots[si];
-            reset_fill(s);
-            if ((rc = ensure_stage(s))) break;
-            s.state = Slot::FILLING;  // reserved: the previous round may still be unlaunched
-            auto& it = items[buf];
-            buf ^= 1;
-            it.clear();
-            uint32_t m = 0;
-            for (uint64_t i = w0; i < w1; ++i) {
-                const uint64_t len_i = i == n - 1 ? last_len : pl;
-                if (a >= len_i && !(a == 0 && len_i == 0)) continue;  // piece already finished
-                const uint64_t clen = std::min<uint64_t>(rlen, len_i - a);
-                it.push_back(vx_files::ReadItem{s.h_stage + (uint64_t)m * pitch, i, a, clen});
-                s.h_offsets[m] = (uint64_t)m * pitch;
-                s.h_lens[m] = (uint32_t)clen;
-                s.h_pidx[m] = (uint32_t)(i - first);
-                s.h_poff[m] = a;
-                s.h_tlen[m] = len_i;
-                ++m;
-            }
-            if (m == 0) {
-                s.state = Slot::FREE;
-                continue;
-            }
-            s.bytes = (uint64_t)(m - 1) * pitch + s.h_lens[m - 1];
-            const auto t_c = clk::now();
-            rd.start(it);
-            rc = enqueue();  // the previous round, while this one reads
-            rd.wait();
-            const auto t_d = clk::now();
-            prev = Pending{si, m, k > 0};
-            if (trace)
-                std::fprintf(stderr, "vx round %zu slot %d at %.2f: wait %.2f prep %.2f read+enqueue %.2f (%.1f GiB/s)\n",
-                             (size_t)k, si, ms(t_call, t_a), ms(t_a, t_b), ms(t_b, t_c), ms(t_c, t_d),
-                             s.bytes / (ms(t_c, t_d) * 1e-3) / (1 << 30));
-        }
+        if (trace)
+            std::fprintf(stderr,
+                         "vx round %zu slot %d at %.2f: slots+reads %.2f read wait %.2f enqueue %.2f (%zu reading)\n",
+                         ne, r.si, ms(t_call, t_a), ms(t_a, t_b), ms(t_b, t_c), ms(t_c, clk::now()), nr - ne - 1);
     }
-    if (!rc) rc = enqueue();
-    for (auto& sl : c->slots)  // a round read but never launched (error path)
+    rd.wait();  // error path: no read may still target a stage
+    for (auto& sl : c->slots)  // rounds read but never launched (error path)
         if (sl.state == Slot::FILLING) {
             reset_fill(sl);
             sl.state = Slot::FREE;
         }
     rc = cp.finish(fv.matched_out, nullptr, rc);
+    if (trace && !tev.empty()) {
+        float t0 = 0, a = 0, b = 0;
+        size_t k = 0;
+        for (const Round& r : rounds) {
+            if (r.m == 0) continue;
+            if (2 * k + 1 >= tev.size()) break;
+            (void)hipEventElapsedTime(&a, tev[0], tev[2 * k]);
+            (void)hipEventElapsedTime(&b, tev[0], tev[2 * k + 1]);
+            std::fprintf(stderr, "vx copy %zu: %.3f -> %.3f ms (%.3f ms, ~%.1f GiB/s) gap %.3f\n", k, a, b, b - a,
+                         r.bytes / ((b - a) * 1e-3) / (1 << 30), a - t0);
+            t0 = b;
+            ++k;
+        }
+        for (hipEvent_t e : tev)
+            if (e) (void)hipEventDestroy(e);
+    }
     if (!rc)
         for (uint64_t i = 0; i < cnt; ++i)
             if (fv.bad[i]) fv.matched_out[i] = 0;
@@ -1336,7 +1397,7 @@ int batch_chunked(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, c
                 s.h_poff[r] = a;
                 s.h_tlen[r] = is_last ? Llast : L;
             }
-            rc = cp.round(si, m, k > 0, [&](Slot& sl, hipStream_t st) {
+            rc = cp.round(si, m, k > 0, false, [&](Slot& sl, hipStream_t st) {
                 if (full_rows && hipMemcpy2DAsync(sl.d_arena, dpitch, base + w0 * hs + a, hs, width, full_rows,
                                                   hipMemcpyHostToDevice, st) != hipSuccess)
                     return fail(VX_EDEVICE, "batch: chunk 2D H2D failed");
@@ -1449,7 +1510,7 @@ int batch_chunked_gather(vx_ctx* c, const uint32_t* lens, const uint8_t* expecte
             for (const auto& pa : act) lane(pa.first, pa.second);
             while (next < n && m < W && (bytes < target || m == 0)) lane(order[next++], 0);
             act.swap(keep);
-            rc = cp.round(si, m, continues, gather_copy(m, tiles));
+            rc = cp.round(si, m, continues, true, gather_copy(m, tiles));
         }
         return cp.finish(matched_out, digests_out, rc);
     }
@@ -1484,7 +1545,7 @@ int batch_chunked_gather(vx_ctx* c, const uint32_t* lens, const uint8_t* expecte
                 ++m;
             }
             if (m == 0) continue;
-            rc = cp.round(si, m, k > 0, gather_copy(m, tiles));
+            rc = cp.round(si, m, k > 0, true, gather_copy(m, tiles));
         }
         cp.end_window();
     }
@@ -1621,8 +1682,7 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
     const std::vector<vx_files::FileSpan> fs = vx_files::layout(file_lengths, nfiles, piece_length);
     std::vector<int> fds(nfiles, -1);
     for (size_t f = 0; f < nfiles; ++f) fds[f] = open(paths[f], O_RDONLY | O_CLOEXEC);
-    const int nthreads = io_threads ? (int)io_threads
-                                    : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    const int nthreads = io_threads ? (int)io_threads : (int)std::max(1u, std::min(16u, usable_cpus()));
     std::vector<uint8_t> bad(count, 0);
     std::memset(matched_out, 0, count);
     {

@@ -19,6 +19,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -111,15 +112,26 @@ inline bool read_range(const std::vector<FileSpan>& fs, const std::vector<int>& 
     return at == (int64_t)it.len;  // short: the files end before the piece does
 }
 
-// A fixed pool of reader threads; run(items) preads every item, marking
-// bad[piece - first] = 1 on any I/O error or short read, and returns when all
-// are done.  `first` is the first piece of the verified range.
+// A fixed pool of reader threads working through a FIFO of read jobs (one
+// job = one round's items).  Workers always take the oldest job's next item,
+// so jobs finish roughly in submission order, and a worker never idles while
+// any submitted item is unread: the re-verify keeps several rounds queued so
+// the reads run back to back however the copies are paced.
+// An item that fails or reads short marks bad[piece - first] = 1.  `first`
+// is the first piece of the verified range.
 class Readers {
   public:
     Readers(int n, const std::vector<FileSpan>& fs, const std::vector<int>& fds, uint32_t piece_length,
             uint8_t* bad, uint64_t first = 0)
         : fs_(fs), fds_(fds), pl_(piece_length), bad_(bad), first_(first) {
-        for (int t = 0; t < n; ++t) th_.emplace_back([this] { loop(); });
+        for (int t = 0; t < n; ++t) {
+            try {
+                th_.emplace_back([this] { loop(); });
+            } catch (...) {  // no more threads: the ones already started do the reads
+                break;
+            }
+        }
+        if (th_.empty()) inline_ = true;  // not even one: submit() reads on the caller's thread
     }
     ~Readers() {
         {
@@ -129,58 +141,76 @@ class Readers {
         cv_.notify_all();
         for (auto& t : th_) t.join();
     }
-    // The caller may rebuild `items` as soon as run() returns, so a worker
-    // takes an item only under the lock and only while the generation it woke
-    // for is still the current one: main waits in run() until every taken
-    // item is done, so the vector is stable while any worker reads it.  (A
-    // lock-free counter let a worker that woke late for a finished
-    // generation index the vector while the caller was refilling it.)
-    void run(const std::vector<ReadItem>& items) {
-        start(items);
-        wait();
-    }
-    // start() hands `items` to the workers and returns; the caller must keep
-    // the vector unchanged until wait() returns, and wait() before the next
-    // start().  (The re-verify enqueues round k while round k+1 reads.)
-    void start(const std::vector<ReadItem>& items) {
-        if (items.empty()) return;
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            items_ = &items;
-            next_ = 0;
-            count_ = items.size();
-            left_ = items.size();
-            ++gen_;
+    // Queue `items` and return its ticket.  The caller keeps the vector
+    // unchanged until wait(ticket) (or wait()) has returned: a worker indexes
+    // it only under the lock and only while the job has untaken items.
+    uint64_t submit(const std::vector<ReadItem>& items) {
+        std::unique_lock<std::mutex> g(mu_);
+        const uint64_t id = base_ + jobs_.size();
+        jobs_.push_back(Job{&items, 0, items.size()});
+        if (inline_) {
+            g.unlock();
+            std::vector<Seg> segs;
+            for (const ReadItem& it : items)
+                if (!read_range(fs_, fds_, pl_, it, segs)) bad_[it.piece - first_] = 1;
+            g.lock();
+            jobs_[id - base_].left = 0;
+            jobs_[id - base_].next = items.size();
+            retire();
+            return id;
         }
+        if (items.empty()) retire();
+        g.unlock();
         cv_.notify_all();
+        return id;
     }
+    // Block until job `ticket` is read.
+    void wait(uint64_t ticket) {
+        std::unique_lock<std::mutex> g(mu_);
+        done_cv_.wait(g, [&] { return ticket < base_ || jobs_[ticket - base_].left == 0; });
+    }
+    // Block until every submitted job is read.
     void wait() {
         std::unique_lock<std::mutex> g(mu_);
-        done_cv_.wait(g, [&] { return left_ == 0; });
+        done_cv_.wait(g, [&] { return jobs_.empty(); });
     }
+    void run(const std::vector<ReadItem>& items) { wait(submit(items)); }
+    // Kept for the whole-piece path: one job at a time.
+    void start(const std::vector<ReadItem>& items) { (void)submit(items); }
 
   private:
+    struct Job {
+        const std::vector<ReadItem>* items;
+        size_t next, left;
+    };
+    // Drop finished jobs from the front (mu_ held); ids stay base_ + index.
+    void retire() {
+        while (!jobs_.empty() && jobs_.front().left == 0) {
+            jobs_.pop_front();
+            ++base_;
+        }
+        done_cv_.notify_all();
+    }
+    // The oldest job with an untaken item (mu_ held), or -1.
+    long pick() const {
+        for (size_t j = 0; j < jobs_.size(); ++j)
+            if (jobs_[j].next < jobs_[j].items->size()) return (long)j;
+        return -1;
+    }
     void loop() {
         std::vector<Seg> segs;
-        uint64_t seen = 0;
+        std::unique_lock<std::mutex> g(mu_);
         for (;;) {
-            {
-                std::unique_lock<std::mutex> g(mu_);
-                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
-            }
-            for (;;) {
-                const ReadItem* it;
-                {
-                    std::lock_guard<std::mutex> g(mu_);
-                    if (gen_ != seen || next_ >= count_) break;  // never touches a finished vector
-                    it = &(*items_)[next_++];
-                }
-                if (!read_range(fs_, fds_, pl_, *it, segs)) bad_[it->piece - first_] = 1;
-                std::lock_guard<std::mutex> g(mu_);
-                if (--left_ == 0) done_cv_.notify_all();
-            }
+            cv_.wait(g, [&] { return stop_ || pick() >= 0; });
+            if (stop_) return;
+            const uint64_t id = base_ + (uint64_t)pick();
+            Job& j = jobs_[id - base_];
+            const ReadItem& it = (*j.items)[j.next++];
+            g.unlock();
+            const bool ok = read_range(fs_, fds_, pl_, it, segs);
+            g.lock();
+            if (!ok) bad_[it.piece - first_] = 1;
+            if (--jobs_[id - base_].left == 0) retire();  // the job cannot have retired: left was > 0
         }
     }
 
@@ -192,10 +222,9 @@ class Readers {
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
-    bool stop_ = false;
-    uint64_t gen_ = 0, left_ = 0;
-    const std::vector<ReadItem>* items_ = nullptr;
-    uint64_t next_ = 0, count_ = 0;
+    bool stop_ = false, inline_ = false;
+    std::deque<Job> jobs_;
+    uint64_t base_ = 0;  // id of jobs_.front()
 };
 
 }  // namespace vx_files
