@@ -2,7 +2,11 @@
 // vx_verify_files): many back-to-back run() generations whose item vector the
 // caller rebuilds (and regrows) between runs; then the pipelined form
 // verify_whole / verify_chunked use (start(g), check generation g-1's bytes
-// while g reads into the other stage, wait(g); two item vectors alternating).
+// while g reads into the other stage, wait(g); two item vectors alternating);
+// then the queued form the re-verify uses since round 2 (submit() up to three
+// jobs ahead, wait(ticket) in order with an occasional later ticket first,
+// empty jobs mixed in, each job checked while later ones read), and the same
+// with a zero-thread pool (reads inline in submit()).
 // Every item must land the right file bytes.  Built plain and with
 // -fsanitize=thread by tests/test_native_cpu.py; exit 0 = ok.
 //
@@ -79,6 +83,37 @@ int main(int argc, char** argv) {
             rd.wait();
         }
         if (gens > 0) check(items2[(gens - 1) & 1]);
+
+        // queued: a ring of 4 jobs, up to 3 in flight past the one awaited
+        auto queued = [&](vx_files::Readers& r, int njobs) {
+            constexpr int K = 4;
+            std::vector<vx_files::ReadItem> ring[K];
+            std::vector<uint8_t> st[K];
+            uint64_t ticket[K] = {};
+            for (auto& v : st) v.resize((size_t)pl * 64);
+            int next = 0;
+            for (int g = 0; g < njobs; ++g) {
+                for (; next < njobs && next <= g + K - 1; ++next) {
+                    auto& its = ring[next % K];
+                    its.clear();
+                    its.shrink_to_fit();
+                    const uint32_t m = rng() % 8 == 0 ? 0 : 1 + rng() % 64;  // some empty jobs
+                    const uint32_t base = rng() % (npieces - 64);
+                    for (uint32_t k = 0; k < m; ++k) {
+                        const uint32_t a = (uint32_t)(rng() % 4) * 512;
+                        its.push_back(vx_files::ReadItem{st[next % K].data() + (size_t)k * pl, base + k, a, pl - a});
+                    }
+                    ticket[next % K] = r.submit(its);
+                }
+                if (g + 1 < next && rng() % 5 == 0) r.wait(ticket[(g + 1) % K]);  // a later job first
+                r.wait(ticket[g % K]);
+                check(ring[g % K]);
+            }
+            r.wait();
+        };
+        queued(rd, gens);
+        vx_files::Readers inline_rd(0, fs, fds, pl, bad.data(), 0);
+        queued(inline_rd, 200);
     }
     close(fds[0]);
     for (uint8_t b : bad) errors += b;

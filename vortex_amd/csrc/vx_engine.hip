@@ -922,8 +922,12 @@ struct FileVerify {
     }
     int free_slot() {
         for (;;) {
-            for (int k = 0; k < (int)c->slots.size(); ++k)
+            bool inflight = false;
+            for (int k = 0; k < (int)c->slots.size(); ++k) {
                 if (c->slots[k].state == Slot::FREE) return k;
+                inflight |= c->slots[k].state == Slot::INFLIGHT;
+            }
+            if (!inflight) return fail(VX_EDEVICE, "vx_verify_files: no slot to wait for");
             int rc = reap(c, true);
             consume();
             if (rc) return rc;
@@ -944,63 +948,78 @@ uint64_t verify_chunk_for(const vx_ctx* c, uint64_t count) {
 }
 
 // Both verify pieces [first, end) of an n-piece torrent; tags, bad[] and
-// matched_out are indexed from `first`.  Both read slot k+1 while slot k is
-// launched (see verify_chunked).
+// matched_out are indexed from `first`.  Both queue reads up to
+// `verify_readahead` slots ahead of the slot being launched (see
+// verify_chunked).
 int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl, uint64_t total, uint64_t first,
                  uint64_t end) {
     vx_ctx* c = fv.c;
     const uint64_t stride = align_up(pl, kAlign);
     const uint64_t last_len = total - (n - 1) * (uint64_t)pl;
-    std::vector<vx_files::ReadItem> items[2];
-    int buf = 0, prev = -1;
-    auto launch_prev = [&]() -> int {
-        if (prev < 0) return 0;
-        int r = launch_slot(c, prev);
-        prev = -1;
-        if (!r) r = reap(c, false);
-        fv.consume();
-        return r;
+    const size_t nslots = c->slots.size();
+    const size_t depth =
+        c->verify_overlap && nslots > 1 ? std::min<size_t>(std::max<uint32_t>(1, c->verify_readahead), nslots - 1) : 0;
+    std::vector<std::vector<vx_files::ReadItem>> items(nslots);
+    struct Queued {
+        int si;
+        uint64_t ticket;
     };
+    std::deque<Queued> q;  // slots read or reading, in piece order, not yet launched
     uint64_t next = first;
     int rc = 0;
-    while (next < end && !rc) {
-        if ((c->slots.size() < 2 || !c->verify_overlap) && (rc = launch_prev())) break;  // one slot: nothing to overlap with
-        const int si = fv.free_slot();
-        if (si < 0) {
-            rc = si;
-            break;
+    while ((next < end || !q.empty()) && !rc) {
+        // The slot to launch next may wait for a free slot; later ones take
+        // only a slot that is free now.
+        while (next < end && q.size() <= depth) {
+            int si = -1;
+            if (q.empty()) {
+                si = fv.free_slot();
+                if (si < 0) rc = si;
+            } else {
+                rc = reap(c, false);
+                fv.consume();
+                for (int k = 0; k < (int)nslots && !rc; ++k)
+                    if (c->slots[k].state == Slot::FREE) {
+                        si = k;
+                        break;
+                    }
+            }
+            if (rc || si < 0) break;
+            Slot& s = c->slots[si];
+            reset_fill(s);
+            if ((rc = ensure_stage(s))) break;
+            s.state = Slot::FILLING;  // reserved until launched
+            const uint64_t cap = std::min<uint64_t>(s.cap, std::max<uint64_t>(1, s.arena_cap / stride));
+            const uint64_t lo = next, hi = std::min<uint64_t>(end, next + cap);
+            auto& it = items[si];
+            it.clear();
+            for (uint64_t i = lo; i < hi; ++i) {
+                const uint32_t len = (uint32_t)(i == n - 1 ? last_len : pl);
+                const uint32_t k = (uint32_t)(i - lo);
+                it.push_back(vx_files::ReadItem{s.h_stage + k * stride, i, 0, len});
+                s.h_offsets[k] = k * stride;
+                s.h_lens[k] = len;
+                if (len != s.h_lens[0]) s.uniform = false;
+                std::memcpy(s.h_expected + (size_t)k * 20, fv.expected + 20 * i, 20);
+                s.tags.push_back(i - first);
+            }
+            s.n = (uint32_t)(hi - lo);
+            s.has_expected = true;
+            s.bytes = (hi - lo - 1) * stride + s.h_lens[s.n - 1];
+            s.runs.push_back(Run{0, s.bytes});
+            q.push_back(Queued{si, rd.submit(it)});
+            next = hi;
         }
-        Slot& s = c->slots[si];
-        reset_fill(s);
-        if ((rc = ensure_stage(s))) break;
-        s.state = Slot::FILLING;  // reserved while the previous slot may still be unlaunched
-        const uint64_t cap = std::min<uint64_t>(s.cap, std::max<uint64_t>(1, s.arena_cap / stride));
-        const uint64_t lo = next, hi = std::min<uint64_t>(end, next + cap);
-        auto& it = items[buf];
-        buf ^= 1;
-        it.clear();
-        for (uint64_t i = lo; i < hi; ++i) {
-            const uint32_t len = (uint32_t)(i == n - 1 ? last_len : pl);
-            const uint32_t k = (uint32_t)(i - lo);
-            it.push_back(vx_files::ReadItem{s.h_stage + k * stride, i, 0, len});
-            s.h_offsets[k] = k * stride;
-            s.h_lens[k] = len;
-            if (len != s.h_lens[0]) s.uniform = false;
-            std::memcpy(s.h_expected + (size_t)k * 20, fv.expected + 20 * i, 20);
-            s.tags.push_back(i - first);
-        }
-        s.n = (uint32_t)(hi - lo);
-        s.has_expected = true;
-        s.bytes = (hi - lo - 1) * stride + s.h_lens[s.n - 1];
-        s.runs.push_back(Run{0, s.bytes});
-        rd.start(it);
-        rc = launch_prev();  // the previous slot, while this one reads
-        rd.wait();
-        prev = si;
-        next = hi;
+        if (rc || q.empty()) break;
+        const Queued head = q.front();
+        q.pop_front();
+        rd.wait(head.ticket);
+        rc = launch_slot(c, head.si);
+        if (!rc) rc = reap(c, false);
+        fv.consume();
     }
-    if (!rc) rc = launch_prev();
-    for (auto& sl : c->slots)  // a slot read but never launched (error path)
+    rd.wait();  // error path: no read may still target a stage
+    for (auto& sl : c->slots)  // slots read but never launched (error path)
         if (sl.state == Slot::FILLING) {
             reset_fill(sl);
             sl.state = Slot::FREE;
