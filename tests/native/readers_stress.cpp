@@ -6,7 +6,10 @@
 // then the queued form the re-verify uses since round 2 (submit() up to three
 // jobs ahead, wait(ticket) in order with an occasional later ticket first,
 // empty jobs mixed in, each job checked while later ones read), and the same
-// with a zero-thread pool (reads inline in submit()).
+// with a zero-thread pool (reads inline in submit()); then whole-piece runs
+// (vx_files::Runs) over a multi-file layout with an empty, a missing and a
+// truncated file: every piece lands the concatenated bytes or is marked bad
+// exactly when the per-piece walk would fail.
 // Every item must land the right file bytes.  Built plain and with
 // -fsanitize=thread by tests/test_native_cpu.py; exit 0 = ok.
 //
@@ -18,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <string>
 #include <vector>
 
 #include "vx_files.hpp"
@@ -117,6 +121,60 @@ int main(int argc, char** argv) {
     }
     close(fds[0]);
     for (uint8_t b : bad) errors += b;
+
+    {  // coalesced runs over several files
+        const uint32_t rpl = 1024;
+        const std::string base = std::string(argv[1]) + ".mf";
+        // declared lengths; file 3 is never created (missing), file 5 is written 3000 bytes short
+        const std::vector<uint64_t> flen{3 * rpl + 100, 0, 5 * rpl - 100, 9 * rpl, 2 * rpl + 500, 40 * rpl + 37};
+        const size_t missing = 3, truncated = 5, cut = 3000;
+        std::vector<uint8_t> all;
+        std::vector<int> mfds;
+        for (size_t f = 0; f < flen.size(); ++f) {
+            std::vector<uint8_t> d(flen[f]);
+            for (auto& b : d) b = (uint8_t)rng();
+            all.insert(all.end(), d.begin(), d.end());
+            const std::string path = base + std::to_string(f);
+            if (f != missing) {
+                FILE* g = std::fopen(path.c_str(), "wb");
+                const size_t w = f == truncated ? d.size() - cut : d.size();
+                if (!g || (w && std::fwrite(d.data(), 1, w, g) != w)) return 2;
+                std::fclose(g);
+            }
+            mfds.push_back(open(path.c_str(), O_RDONLY));
+        }
+        const std::vector<vx_files::FileSpan> mfs = vx_files::layout(flen.data(), flen.size(), rpl);
+        const uint64_t total = all.size(), n = (total + rpl - 1) / rpl;
+        std::vector<uint64_t> fstart{0};
+        for (uint64_t L : flen) fstart.push_back(fstart.back() + L);
+        for (uint64_t max_bytes : {(uint64_t)0, (uint64_t)4 * rpl, (uint64_t)1 << 20}) {
+            std::vector<uint8_t> mbad(n, 0), st(n * rpl, 0);
+            std::vector<vx_files::ReadItem> its;
+            {
+                vx_files::Readers r(3, mfs, mfds, rpl, mbad.data(), 0);
+                vx_files::Runs runs = r.runs(max_bytes);
+                for (uint64_t i = 0; i < n; ++i) runs.add(its, st.data() + i * rpl, i, std::min<uint64_t>(rpl, total - i * rpl));
+                r.wait(r.submit(its));
+            }
+            if (max_bytes >= (1u << 20) && its.size() >= n / 2) ++errors;  // runs did not coalesce
+            for (uint64_t i = 0; i < n; ++i) {
+                const uint64_t a = i * rpl, b = std::min<uint64_t>(total, a + rpl);
+                bool fails = false;  // the walk fails if the piece touches the missing file or the cut tail
+                for (size_t f = 0; f < flen.size(); ++f) {
+                    const uint64_t lo = std::max(a, fstart[f]), hi = std::min(b, fstart[f + 1]);
+                    if (lo >= hi) continue;
+                    if (f == missing) fails = true;
+                    if (f == truncated && hi > fstart[f + 1] - cut) fails = true;
+                }
+                if (fails != (mbad[i] != 0)) ++errors;
+                if (!fails && std::memcmp(st.data() + a, all.data() + a, b - a) != 0) ++errors;
+            }
+        }
+        for (size_t f = 0; f < flen.size(); ++f) {
+            if (mfds[f] >= 0) close(mfds[f]);
+            std::remove((base + std::to_string(f)).c_str());
+        }
+    }
     std::printf("{\"generations\": %d, \"errors\": %d}\n", gens, errors);
     return errors == 0 ? 0 : 1;
 }

@@ -155,7 +155,8 @@ struct vx_ctx {
     int verify_ramp = 1;  // ramp depth d: first/last rounds C / 2^(d+1) (0 = off)
     uint64_t verify_chunked_above = 0;
     bool verify_overlap = true;  // read round k+1 while round k is enqueued (VX_VERIFY_OVERLAP)
-    uint32_t verify_readahead = 2;  // chunked re-verify: rounds read ahead of the enqueue (VX_VERIFY_READAHEAD)
+    uint32_t verify_readahead = 2;  // re-verify: rounds / slots read ahead of the enqueue (VX_VERIFY_READAHEAD)
+    bool verify_coalesce = true;    // whole-piece re-verify: one pread per run of pieces in one file (VX_VERIFY_COALESCE)
     uint64_t chunk_rounds = 0;  // chunk rounds launched (vx_tuning_chunk_rounds)
     // Per-piece device rows of the chunk paths (state | expected | digest |
     // verdict), kept across calls and grown on demand: allocating them per
@@ -726,6 +727,7 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (const char* m = std::getenv("VX_VERIFY_RAMP")) c->verify_ramp = std::max(0, std::min(5, std::atoi(m)));
     if (const char* m = std::getenv("VX_VERIFY_CHUNKED_ABOVE")) c->verify_chunked_above = std::strtoull(m, nullptr, 0);
     if (const char* m = std::getenv("VX_VERIFY_OVERLAP")) c->verify_overlap = std::atoi(m) != 0;
+    if (const char* m = std::getenv("VX_VERIFY_COALESCE")) c->verify_coalesce = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_VERIFY_READAHEAD")) c->verify_readahead = (uint32_t)std::max(1, std::atoi(m));
     int rc = set_device(c);
     if (!rc && c->h2d_mode == 3 && hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess)
@@ -965,6 +967,9 @@ int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl,
         uint64_t ticket;
     };
     std::deque<Queued> q;  // slots read or reading, in piece order, not yet launched
+    // Runs of whole pieces inside one file go out as one pread of up to 4 MiB
+    // (vx_files::Runs; 16 KiB pieces were pread-bound); VX_VERIFY_COALESCE=0 reads piece by piece.
+    vx_files::Runs runs = rd.runs(c->verify_coalesce ? 4ull << 20 : 0);
     uint64_t next = first;
     int rc = 0;
     while ((next < end || !q.empty()) && !rc) {
@@ -996,7 +1001,7 @@ int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl,
             for (uint64_t i = lo; i < hi; ++i) {
                 const uint32_t len = (uint32_t)(i == n - 1 ? last_len : pl);
                 const uint32_t k = (uint32_t)(i - lo);
-                it.push_back(vx_files::ReadItem{s.h_stage + k * stride, i, 0, len});
+                runs.add(it, s.h_stage + k * stride, i, len);
                 s.h_offsets[k] = k * stride;
                 s.h_lens[k] = len;
                 if (len != s.h_lens[0]) s.uniform = false;

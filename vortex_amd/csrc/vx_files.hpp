@@ -87,12 +87,18 @@ inline bool read_full(int fd, uint8_t* dst, int64_t off, int64_t len) {
 }
 
 // One read job: bytes [start, start+len) of piece `piece` (a sub-range of
-// the piece's concatenated segments) into dst.
+// the piece's concatenated segments) into dst.  A run item (file >= 0) is
+// instead `pieces` consecutive pieces lying wholly inside file `file` from
+// byte file_off on, landing back to back at dst (piece length apart): one
+// pread for all of them (see Runs).
 struct ReadItem {
     uint8_t* dst;
     uint64_t piece;
     uint64_t start;
     uint64_t len;
+    int32_t file = -1;
+    uint32_t pieces = 1;
+    int64_t file_off = 0;
 };
 
 // Bytes [start, start+len) of a piece, mapped onto its file segments.
@@ -111,6 +117,57 @@ inline bool read_range(const std::vector<FileSpan>& fs, const std::vector<int>& 
     }
     return at == (int64_t)it.len;  // short: the files end before the piece does
 }
+
+// Coalesced reads for whole pieces.  A piece that lies wholly inside one
+// file has a single segment in check_piece_hash_sync's walk
+// (file_store.rs:240-298): (piece - start_piece) * piece_length -
+// start_offset bytes into that file, the piece's length long.  Consecutive
+// such pieces of one file are therefore contiguous in it, and a slot that
+// stages pieces piece_length apart can pread the whole run at once instead of
+// piece by piece (with 16 KiB pieces the per-piece preads were the bound).
+// Pieces that straddle files, or sit in a file that failed to open, keep the
+// per-piece walk; a run whose pread fails or reads short is re-read piece by
+// piece, so every verdict is the walk's.
+class Runs {
+  public:
+    Runs(const std::vector<FileSpan>& fs, const std::vector<int>& fds, uint32_t piece_length, uint64_t max_bytes)
+        : fs_(fs), fds_(fds), pl_(piece_length), max_(max_bytes) {}
+    // Append piece `piece` (len bytes, staged at dst) to `out`, extending the
+    // last item when it is a run the piece continues.  Pieces must come in
+    // increasing order.
+    void add(std::vector<ReadItem>& out, uint8_t* dst, uint64_t piece, uint64_t len) {
+        const int64_t a = (int64_t)piece * pl_, b = a + (int64_t)len;
+        while (f_ < fs_.size() && a >= file_start(f_) + fs_[f_].len) ++f_;
+        const bool inside = f_ < fs_.size() && len > 0 && a >= file_start(f_) && b <= file_start(f_) + fs_[f_].len &&
+                            fds_[f_] >= 0;
+        if (!inside || max_ == 0) {
+            out.push_back(ReadItem{dst, piece, 0, len});
+            return;
+        }
+        const int64_t off = a - file_start(f_);
+        if (!out.empty()) {
+            ReadItem& r = out.back();
+            if (r.file == (int32_t)f_ && r.piece + r.pieces == piece && r.len == (uint64_t)r.pieces * pl_ &&
+                r.file_off + (int64_t)r.len == off && r.dst + r.len == dst && r.len + len <= max_) {
+                r.len += len;
+                r.pieces += 1;
+                return;
+            }
+        }
+        ReadItem r{dst, piece, 0, len};
+        r.file = (int32_t)f_;
+        r.file_off = off;
+        out.push_back(r);
+    }
+
+  private:
+    int64_t file_start(size_t f) const { return fs_[f].start_piece * (int64_t)pl_ + fs_[f].start_offset; }
+    const std::vector<FileSpan>& fs_;
+    const std::vector<int>& fds_;
+    const uint32_t pl_;
+    const uint64_t max_;
+    size_t f_ = 0;
+};
 
 // A fixed pool of reader threads working through a FIFO of read jobs (one
 // job = one round's items).  Workers always take the oldest job's next item,
@@ -151,8 +208,7 @@ class Readers {
         if (inline_) {
             g.unlock();
             std::vector<Seg> segs;
-            for (const ReadItem& it : items)
-                if (!read_range(fs_, fds_, pl_, it, segs)) bad_[it.piece - first_] = 1;
+            for (const ReadItem& it : items) read_item(it, segs);
             g.lock();
             jobs_[id - base_].left = 0;
             jobs_[id - base_].next = items.size();
@@ -175,6 +231,8 @@ class Readers {
         done_cv_.wait(g, [&] { return jobs_.empty(); });
     }
     void run(const std::vector<ReadItem>& items) { wait(submit(items)); }
+    // A run builder over this pool's files (whole-piece slots).
+    Runs runs(uint64_t max_bytes) const { return Runs(fs_, fds_, pl_, max_bytes); }
     // Kept for the whole-piece path: one job at a time.
     void start(const std::vector<ReadItem>& items) { (void)submit(items); }
 
@@ -183,6 +241,22 @@ class Readers {
         const std::vector<ReadItem>* items;
         size_t next, left;
     };
+    // Chunk rounds of one piece may be read by two workers at once (queued
+    // jobs), so the bad flag is stored atomically; the caller reads it after
+    // wait(), which orders it through mu_.
+    void mark_bad(uint64_t piece) { __atomic_store_n(&bad_[piece - first_], (uint8_t)1, __ATOMIC_RELAXED); }
+    void read_item(const ReadItem& it, std::vector<Seg>& segs) {
+        if (it.file >= 0 && read_full(fds_[it.file], it.dst, it.file_off, (int64_t)it.len)) return;
+        if (it.file < 0) {
+            if (!read_range(fs_, fds_, pl_, it, segs)) mark_bad(it.piece);
+            return;
+        }
+        for (uint32_t k = 0; k < it.pieces; ++k) {  // the run failed: piece by piece, as the walk reads
+            const uint64_t len = k + 1 < it.pieces ? pl_ : it.len - (uint64_t)k * pl_;
+            const ReadItem one{it.dst + (uint64_t)k * pl_, it.piece + k, 0, len};
+            if (!read_range(fs_, fds_, pl_, one, segs)) mark_bad(one.piece);
+        }
+    }
     // Drop finished jobs from the front (mu_ held); ids stay base_ + index.
     void retire() {
         while (!jobs_.empty() && jobs_.front().left == 0) {
@@ -207,9 +281,8 @@ class Readers {
             Job& j = jobs_[id - base_];
             const ReadItem& it = (*j.items)[j.next++];
             g.unlock();
-            const bool ok = read_range(fs_, fds_, pl_, it, segs);
+            read_item(it, segs);
             g.lock();
-            if (!ok) bad_[it.piece - first_] = 1;
             if (--jobs_[id - base_].left == 0) retire();  // the job cannot have retired: left was > 0
         }
     }
