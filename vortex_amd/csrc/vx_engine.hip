@@ -970,9 +970,11 @@ int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl,
     // Runs of whole pieces inside one file go out as one pread of up to 4 MiB
     // (vx_files::Runs; 16 KiB pieces were pread-bound); VX_VERIFY_COALESCE=0 reads piece by piece.
     vx_files::Runs runs = rd.runs(c->verify_coalesce ? 4ull << 20 : 0);
-    // Head ramp: nothing overlaps the first slot's read, so the first slots
-    // take 1/2^L, ..., 1/4, 1/2 of a full slot's pieces, the first one
-    // <= 64 MiB (VX_VERIFY_RAMP=0 turns it off; as for chunks, §6.3).
+    // Ramps: nothing overlaps the first slot's read or the last slot's copy
+    // and kernel, so the first slots take 1/2^L, ..., 1/4, 1/2 of a full
+    // slot's pieces, the first one <= 64 MiB, and the last full slot's worth
+    // is split in halves down to that size (VX_VERIFY_RAMP=0 turns both off;
+    // as for chunks, §6.3).
     const uint64_t cap_full =
         std::min<uint64_t>(c->slots[0].cap, std::max<uint64_t>(1, c->slots[0].arena_cap / stride));
     int ramp = 0;
@@ -1003,7 +1005,9 @@ int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl,
             reset_fill(s);
             if ((rc = ensure_stage(s))) break;
             s.state = Slot::FILLING;  // reserved until launched
-            const uint64_t cap = filled < ramp ? std::max<uint64_t>(1, cap_full >> (ramp - filled)) : cap_full;
+            uint64_t cap = filled < ramp ? std::max<uint64_t>(1, cap_full >> (ramp - filled)) : cap_full;
+            const uint64_t rem = end - next, smallest = std::max<uint64_t>(1, cap_full >> ramp);
+            if (ramp > 0 && rem <= cap && rem > smallest) cap = std::max(smallest, (rem + 1) / 2);
             ++filled;
             const uint64_t lo = next, hi = std::min<uint64_t>(end, next + cap);
             auto& it = items[si];
