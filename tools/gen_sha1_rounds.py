@@ -226,10 +226,92 @@ def consumer_asm(select: bool, mode: str = "burst", slots: int = 3) -> str:
     return "\n".join(L)
 
 
-def consumer_clobbers(select: bool, mode: str = "burst"):
+FLAG_V, CONS_V = "v88", "v89"  # flags mode: last read of the producer's count; the count we publish
+SPIN_LIMIT = 1 << 22           # polls (s_sleep 1 each, ~64 cycles) before a wait gives up: ~0.1-0.3 s
+
+
+def _spin(label: str, need: str) -> list:
+    """Wait until the producer's published count (LDS dword at %9) is >= the
+    SGPR `need`.  FLAG_V already holds a recent read of it (lgkmcnt settled), so
+    the fast path is v_readfirstlane + compare + branch.  The slow path polls with
+    s_sleep; after SPIN_LIMIT polls it gives up and sets s29 = 1 (the block is then
+    hashed from a stale slot; the exit stores s29 at %9 + 8 for the caller to
+    report as a failed launch)."""
+    return [f".Lvx_{label}%=:", f"v_readfirstlane_b32 s26, {FLAG_V}", f"s_cmp_ge_u32 s26, {need}",
+            f"s_cbranch_scc1 .Lvx_{label}ok%=", "s_add_u32 s28, s28, 1", f"s_cmp_ge_u32 s28, {SPIN_LIMIT}",
+            f"s_cbranch_scc1 .Lvx_{label}bail%=", "s_sleep 1", f"ds_read_b32 {FLAG_V}, %9",
+            "s_waitcnt lgkmcnt(0)", f"s_branch .Lvx_{label}%=", f".Lvx_{label}bail%=:", "s_mov_b32 s29, 1",
+            f".Lvx_{label}ok%=:"]
+
+
+def consumer_flags_asm(select: bool) -> str:
+    """The consumer with an LDS flag handshake instead of s_barrier (3 slots,
+    burst reads).  %9 = LDS byte address of two dwords {prod, cons}: the
+    producer stores prod = j + 1 after block j's slot is written; the consumer
+    stores cons = b + 2 once block b + 1's slot is in registers (end of block b),
+    and the producer writes block j only when cons >= j - 2.  At the top of
+    block b the consumer needs prod >= b + 2 (block b + 1 published) unless b is
+    its last block; the count it tests was read at the top of block b - 1, so
+    in steady state (producer ahead) the wait is one readfirstlane + compare.
+    Other operands as consumer_asm.  On exit the dword at %9 + 8 is 1 if a wait
+    gave up (never in a correct pairing; a bounded wait keeps a protocol bug
+    from hanging the GPU), else 0."""
+    L = [f"v_mov_b32_e64 v{H0 + i}, %{i}" for i in range(5)]
+    L += ["s_mov_b32 s20, 0x5a827999", "s_mov_b32 s21, 0x6ed9eba1", "s_mov_b32 s22, 0x8f1bbcdc",
+          "s_mov_b32 s23, 0xca62c1d6", "s_mov_b32 s24, 0", "s_mov_b32 s28, 0", "s_mov_b32 s29, 0",
+          "s_mov_b32 s27, 1", "s_cmp_eq_u32 %6, 0", "s_cbranch_scc1 .Lvx_end%=",
+          f"ds_read_b32 {FLAG_V}, %9", "s_waitcnt lgkmcnt(0)"]
+    L += _spin("w0", "s27")
+    L += [_read(WA, q, 0) for q in range(20)]
+    L += ["s_waitcnt lgkmcnt(0)", f"v_mov_b32_e64 {CONS_V}, 1", f"ds_write_b32 %9, {CONS_V} offset:4",
+          ".p2align 5", ".Lvx_loop%=:"]
+    for k in range(6):
+        cur = WA if k % 2 == 0 else WB
+        nxt = WB if cur == WA else WA
+        # s27 = b + 2: the count block b + 1 needs, and what we publish at the end
+        L += ["s_add_u32 s27, s24, 2", "s_cmp_gt_u32 s27, %6", f"s_cbranch_scc1 .Lvx_w{k + 1}ok%="]
+        L += _spin(f"w{k + 1}", "s27")
+        L += [f"ds_read_b32 {FLAG_V}, %9", "s_nop 0", ".p2align 3"]
+        body = _block(consumer_regs(cur), "burst", (k + 1) % 3, nxt)
+        if select:
+            L += ["s_cmp_lt_u32 s24, %7", f"s_cbranch_scc0 .Lvx_sel{k}_%=", ".p2align 3"]
+            L += body
+            L += [f"s_branch .Lvx_done{k}_%=", "s_nop 0", ".p2align 3", f".Lvx_sel{k}_%=:"]
+            L += [f"v_mov_b32_e64 v{SAVE0 + i}, v{H0 + i}" for i in range(5)]
+            L += body
+            L += ["v_cmp_lt_u32_e64 vcc, s24, %8"]
+            L += [f"v_cndmask_b32_e64 v{H0 + i}, v{SAVE0 + i}, v{H0 + i}, vcc" for i in range(5)]
+            L += [".p2align 3", f".Lvx_done{k}_%=:"]
+        else:
+            L += body
+        # body ends with lgkmcnt(0): block b + 1's words (and the count read) are in registers
+        L += [f"v_mov_b32_e64 {CONS_V}, s27", f"ds_write_b32 %9, {CONS_V} offset:4",
+              "s_add_u32 s24, s24, 1", "s_cmp_ge_u32 s24, %6", "s_cbranch_scc1 .Lvx_end%=", ".p2align 3"]
+    L += ["s_branch .Lvx_loop%=", ".Lvx_end%=:", f"v_mov_b32_e64 {CONS_V}, s29",
+          f"ds_write_b32 %9, {CONS_V} offset:8", "s_waitcnt lgkmcnt(0)"]
+    L += [f"v_mov_b32_e64 %{i}, v{H0 + i}" for i in range(5)]
+    return "\n".join(L)
+
+
+def consumer_clobbers(select: bool, mode: str = "burst", flags: bool = False):
     v = [f"v{i}" for i in range(H0, SAVE0 + 5 if select else SAVE0)] + ([ADDR] if mode == "burst2" else [])
+    v += [FLAG_V, CONS_V] if flags else []
     v += [f"v{i}" for i in range(WA, (WA if mode == "refill" else WB) + 80)]
-    return v + ["s20", "s21", "s22", "s23", "s24", "s25", "vcc"]
+    return v + ["s20", "s21", "s22", "s23", "s24", "s25", "vcc"] + (["s26", "s27", "s28", "s29"] if flags else [])
+
+
+def write_consumerf_header(path: str) -> None:
+    with open(path, "w") as f:
+        f.write("// GENERATED by tools/gen_sha1_rounds.py --consumerf; do not edit.\n"
+                "// The split kernels' consumer loop with an LDS flag handshake instead of\n"
+                "// s_barrier (3 slots, burst reads; consumer_flags_asm).\n#pragma once\n\n")
+        for name, sel in (("VX_CONSUMERF_ASM", False), ("VX_CONSUMERF_SELECT_ASM", True)):
+            f.write(f"#define {name} \\\n")
+            for line in consumer_flags_asm(sel).splitlines():
+                f.write(f'    "{line}\\n" \\\n')
+            f.write('    ""\n')
+            f.write(f"#define {name}_CLOBBERS " + ", ".join(f'"{r}"' for r in consumer_clobbers(sel, flags=True))
+                    + "\n\n")
 
 
 def write_consumer_header(path: str, mode: str, slots: int = 3) -> None:
@@ -335,6 +417,7 @@ def main():
     ap.add_argument("--consumer", help="write the split kernels' consumer asm header")
     ap.add_argument("--consumer6", help="write the 6-slot, barrier-per-pair consumer header (probe only: "
                                            "no faster in the kernels, DESIGN.md §3.2.1)")
+    ap.add_argument("--consumerf", help="write the flag-handshake consumer header (consumer_flags_asm)")
     ap.add_argument("--mode", default="burst", choices=["refill", "burst", "burst2", "spread"],
                     help="ring-read placement (burst: the kernel's; A/B in DESIGN.md §3.2)")
     a = ap.parse_args()
@@ -348,6 +431,8 @@ def main():
         write_consumer_header(a.consumer, a.mode)
     if a.consumer6:
         write_consumer_header(a.consumer6, a.mode, slots=6)
+    if a.consumerf:
+        write_consumerf_header(a.consumerf)
     if a.header:
         body = emit(ins, final, R.h)
         regs = sorted({r for r in R.h + R.w + R.a + R.c + R.x + R.f + [R.r]}, key=lambda r: int(r[1:]))

@@ -12,6 +12,9 @@
 //   4  as 2 with the producer's VALU as a rolled loop (little instruction fetch)
 //   5  as 2 with the consumer at s_setprio 3
 //   6  as 2 with a 6-slot ring and one barrier per PAIR of blocks (120 KiB LDS)
+//   7  as 2 with no barriers: an LDS flag handshake (producer count / consumer
+//      count, tools/gen_sha1_rounds.py consumer_flags_asm), bounded waits
+//   8  as 7 with the producer passing the flags only (no LDS writes, no VALU)
 // The consumer stamps s_memtime around its whole loop; prints cycles per
 // block (median over pairs) and the wall ns per block.  No HBM traffic.
 #include <hip/hip_runtime.h>
@@ -22,6 +25,7 @@
 
 #include "../../vortex_amd/csrc/sha1_consumer_asm.inc"
 #include "sha1_consumer6_asm.inc"  // python tools/gen_sha1_rounds.py --consumer6 tools/native/sha1_consumer6_asm.inc
+#include "sha1_consumerf_asm.inc"  // python tools/gen_sha1_rounds.py --consumerf tools/native/sha1_consumerf_asm.inc
 
 template <int S>
 struct Ring {
@@ -32,8 +36,41 @@ template <int P>
 __global__ __launch_bounds__(128) void pair(uint32_t nb, uint32_t* out, unsigned long long* cyc) {
     constexpr int S = P == 6 ? 6 : 3;  // 6: barrier per pair of blocks (VX_CONSUMER6_ASM)
     __shared__ Ring<S> lds;
+    __shared__ uint32_t flags[4];  // P >= 7: {prod, cons, consumer gave up, producer gave up}
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (P >= 7) {
+        if (threadIdx.x < 4) flags[threadIdx.x] = 0;
+        __syncthreads();
+    }
+    if (wave == 1 && P >= 7) {  // flag-handshake producer
+        uint32_t x = lane * 0x9E3779B9u, y = 0x12345u + lane;
+        for (uint32_t b = 0; b < nb; ++b) {
+            if (P == 7) {
+#pragma unroll
+                for (int i = 0; i < 70; ++i) {  // 210 VALU
+                    x = __builtin_amdgcn_alignbit(x, x, 31) ^ y;
+                    y = __builtin_amdgcn_bitop3_b32(x, y, 0x5a5a5a5au, 0x96);
+                    x = x + y;
+                }
+            }
+            uint32_t polls = 0;  // slot b % 3 is free once the consumer has read block b - 3
+            while ((int)__hip_atomic_load(&flags[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < (int)b - 2) {
+                __builtin_amdgcn_s_sleep(1);
+                if (++polls > (1u << 22)) {
+                    flags[3] = 1;
+                    break;
+                }
+            }
+            if (P == 7) {
+#pragma unroll
+                for (int q = 0; q < 20; ++q) lds.w[b % S][q][lane] = make_uint4(x + q, y, x ^ q, b);
+            }
+            __hip_atomic_store(&flags[0], b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        out[blockIdx.x * 64 + lane] = x ^ y;
+        return;
+    }
     if (wave == 1) {  // producer
         uint32_t x = lane * 0x9E3779B9u, y = 0x12345u + lane;
         for (uint32_t b = 0; b < nb; ++b) {
@@ -71,8 +108,14 @@ __global__ __launch_bounds__(128) void pair(uint32_t nb, uint32_t* out, unsigned
     const uint32_t addr = (uint32_t)(uintptr_t)&lds.w[0][0][lane];
     const uint32_t addr3 = (uint32_t)(uintptr_t)&lds.w[S == 6 ? 3 : 0][0][lane];
     const uint32_t zero = 0;
+    const uint32_t faddr = (uint32_t)(uintptr_t)&flags[0];
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    if (S == 6)
+    if (P >= 7)
+        asm volatile(VX_CONSUMERF_ASM
+                     : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3), "+v"(h4)
+                     : "v"(addr), "s"(nb), "s"(nb), "v"(zero), "v"(faddr)
+                     : VX_CONSUMERF_ASM_CLOBBERS, "memory");
+    else if (S == 6)
         asm volatile(VX_CONSUMER6_ASM
                      : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3), "+v"(h4)
                      : "v"(addr), "s"(nb), "s"(nb), "v"(zero), "v"(addr3)
@@ -84,7 +127,7 @@ __global__ __launch_bounds__(128) void pair(uint32_t nb, uint32_t* out, unsigned
                      : VX_CONSUMER_ASM_CLOBBERS, "memory");
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     out[blockIdx.x * 64 + lane] = h0 ^ h1 ^ h2 ^ h3 ^ h4;
-    if (lane == 0) cyc[blockIdx.x] = t1 - t0;
+    if (lane == 0) cyc[blockIdx.x] = (P >= 7 && (flags[2] | flags[3])) ? ~0ull : t1 - t0;
 }
 
 template <int P>
@@ -103,6 +146,7 @@ static void run(const char* name, int grid, uint32_t* d, unsigned long long* dc,
     std::vector<unsigned long long> c(grid);
     (void)hipMemcpy(c.data(), dc, grid * 8, hipMemcpyDeviceToHost);
     std::sort(c.begin(), c.end());
+    if (c.back() == ~0ull) std::printf("%s\"%s_GAVE_UP\": 1", comma ? ", " : "", name);
     std::printf("%s\"%s\": {\"cycles_per_block\": %.1f, \"ns_per_block\": %.1f, \"pairs\": %d}", comma ? ", " : "",
                 name, (double)c[grid / 2] / nb, ms * 1e6 / nb, grid);
 }
@@ -119,6 +163,9 @@ int main() {
     run<4>("lds_writes_valu_rolled_loop", 64, d, dc, true);
     run<5>("lds_writes_valu_consumer_prio3", 64, d, dc, true);
     run<6>("lds_writes_valu_6slots_barrier_per_pair", 64, d, dc, true);
+    run<8>("flags_only", 64, d, dc, true);
+    run<7>("flags_lds_writes_valu", 64, d, dc, true);
+    run<7>("flags_lds_writes_valu_2_pairs_per_cu", 512, d, dc, true);
     std::printf("}\n");
     return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
