@@ -374,13 +374,13 @@ def roofline(n: int, plen: int, kern_ms: float, achieved: float, workload: str) 
     achieved/peak/frac: algorithmic bytes per launch / HIP-event launch time
     against the 8 TB/s HBM3E peak — the fraction of the HBM roofline the
     metric asks for.  The kernel is NOT bound by HBM (traffic is 1.0007x the
-    algorithmic bytes, waits < 1 %): it is bound by integer-VALU issue at one
-    wave per SIMD, at a clock the 1,400 W board power cap holds at
-    1.7-2.3 GHz.  `bound` names that; `valu` gives the fraction against the
-    one-wave issue ceiling (one wave64 instruction per 4 cycles per SIMD),
-    the measured multi-wave SIMD rate (3.03 cycles per wave64 instruction
-    with 4 waves, tools/native/valu_probe.hip -> profiles/r01/valu/valu.json)
-    and the SIMD32 hardware rate (2 cycles), all at the nominal 2.4 GHz, plus
+    algorithmic bytes, waits < 1 %): it is bound by integer-VALU issue — 613.5
+    VOP3-encoded ops per 64-byte block, one wave per SIMD, each op holding the
+    SIMD ~4.1 cycles — at the 2.0-2.4 GHz the chip holds under full VALU load.
+    `bound` names that; `valu` gives the fraction against the one-wave issue
+    ceiling (4 cycles per op at the nominal 2.4 GHz), the measured VOP3 rate
+    per SIMD, the measured whole-chip rate of SHA-1's ops at one wave per SIMD
+    (tools/native/energy_probe.hip), the 2-cycle rate only VOP2 ops reach, and
     the PMC cycles per VALU and clock of the committed profile."""
     blocks = (plen + 9 + 63) // 64
     valu_per_block = 613.5  # measured: SQ_INSTS_VALU / waves / blocks (profiles/pmc_traffic.json)
@@ -389,6 +389,23 @@ def roofline(n: int, plen: int, kern_ms: float, achieved: float, workload: str) 
 
     def peak(cycles_per_inst):
         return simds * 64 / cycles_per_inst * f_nom
+
+    # Measured ceilings of this op mix (tools/native/energy_probe.hip):
+    # a VOP3 op (add3/alignbit/bitop3/perm) costs its SIMD ~4.08-4.17 cycles with
+    # one or two waves per SIMD (only VOP2 ops reach 2 cycles), and a stream of
+    # SHA-1's round ops at one wave per SIMD on all 1,024 SIMDs sustains the
+    # chip's wave-op rate at the clock it holds under VALU load (2.17-2.37 GHz).
+    vop3_cyc, stream = 4.08, None
+    try:
+        with open(os.path.join(ROOT, "profiles", "r02", "valu", "energy_probe_run2.json")) as f:
+            ep = json.load(f)
+        vop3_cyc = ep["add3_2_waves_per_simd"]["cycles_per_op"] / 2
+        rates = [ep[k]["chip_Gwaveops_per_s"] for k in ("sha_mix", "sha_mix_again")]
+        stream = {"lo": min(rates), "hi": max(rates),
+                  "clock_GHz": sorted({ep[k]["clock_GHz"] for k in ("sha_mix", "sha_mix_again")})}
+    except (OSError, ValueError, KeyError):
+        pass
+    wave_ops = ops / 64  # wave-instructions per second, whole chip
 
     traffic = load_traffic(workload, n, plen)
     pmc = None
@@ -406,19 +423,35 @@ def roofline(n: int, plen: int, kern_ms: float, achieved: float, workload: str) 
     return {"bound": "valu", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
             "traffic_ratio": round(traffic / (n * plen), 5) if traffic else None,
-            "bound_note": "integer-VALU issue at 1 wave/SIMD under the board power cap, not HBM: frac is the "
-                          "HBM-roofline fraction the metric asks for; the binding roof is in `valu`",
+            "bound_note": "integer-VALU issue (VOP3 ops, one wave per SIMD), not HBM: frac is the HBM-roofline "
+                          "fraction the metric asks for; the binding roof and the kernel's fraction of it are in `valu`",
             "kernel": "sha1_uniform_kernel", "kernel_ms": round(kern_ms, 4),
             "algorithmic_bytes_per_launch": n * plen,
             "valu": {"achieved_Tops": round(ops / 1e12, 2), "valu_per_block": valu_per_block,
                      "one_wave_issue": {"peak_Tops": round(peak(4.0) / 1e12, 2), "frac": round(ops / peak(4.0), 4)},
-                     "multi_wave_measured": {"peak_Tops": round(peak(3.03) / 1e12, 2),
-                                             "frac": round(ops / peak(3.03), 4),
-                                             "source": "profiles/r01/valu/valu.json (4 waves/SIMD)"},
-                     "simd32_hw": {"peak_Tops": round(peak(2.0) / 1e12, 2), "frac": round(ops / peak(2.0), 4)},
+                     "vop3_simd_measured": {"cycles_per_op_per_simd": round(vop3_cyc, 3),
+                                            "peak_Tops": round(peak(vop3_cyc) / 1e12, 2),
+                                            "frac": round(ops / peak(vop3_cyc), 4),
+                                            "source": "profiles/r02/valu/energy_probe_run2.json (2 waves/SIMD)"},
+                     "multi_wave_mixed_measured": {
+                         "peak_Tops": round(peak(3.03) / 1e12, 2), "frac": round(ops / peak(3.03), 4),
+                         "source": "profiles/r01/valu/valu.json (4 waves/SIMD)",
+                         "note": "that probe's loop, as hipcc compiled it, is half VOP2 (v_xor_b32_e32, "
+                                 "v_add_u32_e32), and a VOP2 op takes its SIMD 2 cycles, so the mix beats 4 cycles "
+                                 "per op; this kernel's stream is VOP3: see vop3_simd_measured"},
+                     "stream_ceiling": None if stream is None else {
+                         "achieved_Gwaveops_per_s": round(wave_ops / 1e9, 1),
+                         "ceiling_Gwaveops_per_s": [stream["lo"], stream["hi"]],
+                         "clock_GHz": stream["clock_GHz"],
+                         "frac": [round(wave_ops / 1e9 / stream["hi"], 4), round(wave_ops / 1e9 / stream["lo"], 4)],
+                         "source": "profiles/r02/valu/energy_probe_run*.json: SHA-1 round ops, 1 wave on each of "
+                                   "the 1,024 SIMDs, ~1.5-2 s; the range is the chip's two clock states"},
+                     "simd32_vop2_only": {"peak_Tops": round(peak(2.0) / 1e12, 2), "frac": round(ops / peak(2.0), 4)},
                      "pmc": pmc,
-                     "note": "65,536 pieces = exactly one wave per SIMD; 2 waves/SIMD (131,072 x 128 KiB) "
-                             "ran no faster at the power cap (DESIGN.md §4)"}}
+                     "note": "65,536 pieces = exactly one wave per SIMD. Every SHA-1 op but the schedule's "
+                             "2-input xor and the feed-forward add is VOP3-only on gfx950, and a VOP3 op holds "
+                             "its SIMD ~4.1 cycles however many waves share it, so 2 waves/SIMD (131,072 x "
+                             "128 KiB) run no faster (DESIGN.md §4)"}}
 
 
 def main() -> int:
