@@ -143,6 +143,34 @@ int vx_drain(vx_ctx* ctx, uint32_t timeout_ms);
 /* Pieces submitted but not yet returned by vx_poll. */
 uint64_t vx_pending(const vx_ctx* ctx);
 
+/* ---- observability ------------------------------------------------------
+ * vortex's hashing is invisible to its `metrics` feature (no
+ * hash-time metric; the exported series are pieces_completed,
+ * disk_write_time_ms, buffer_lifetime_ms ..., event_loop.rs:976-993,
+ * buf_pool.rs:149-154).  These counters let the event loop export hash
+ * throughput, mismatches, loop stalls and batch latency.  Cumulative since
+ * vx_create or the last vx_reset_stats; host-side bookkeeping only (a clock
+ * read per batch, none per piece).  Read them from the thread that drives the
+ * context, like every other call. */
+#define VX_STATS_HIST 24
+typedef struct vx_stats {
+    uint64_t pieces_completed;    /* results produced: async completions, host-batch and re-verified pieces */
+    uint64_t pieces_mismatched;   /* of those compared with an expected digest, how many differed        */
+    uint64_t bytes_completed;     /* piece bytes behind pieces_completed                                 */
+    uint64_t batches;             /* whole-piece batches launched (async, host batches, re-verify slots) */
+    uint64_t chunk_rounds;        /* resumable chunk rounds launched (long pieces)  */
+    uint64_t gather_tiles;        /* 64 KiB tiles the gather kernel pulled from registered host buffers  */
+    uint64_t staged_bytes;        /* bytes copied into pinned staging from unregistered caller memory    */
+    uint64_t io_errors;           /* re-verified pieces with a failed or short read (torrent.rs:731-737) */
+    uint64_t submit_stall_ns;     /* time submits waited for a batch to finish (the loop thread blocked) */
+    uint64_t batch_latency_count; /* whole-piece batches harvested                                       */
+    uint64_t batch_latency_sum_us; /* first submit of a batch -> its results harvested, summed           */
+    uint64_t batch_latency_max_us;
+    uint64_t batch_latency_hist[VX_STATS_HIST]; /* batches per [2^k, 2^(k+1)) us; [0] holds < 2 us, the last bucket everything longer */
+} vx_stats;
+int vx_get_stats(const vx_ctx* ctx, vx_stats* out);
+int vx_reset_stats(vx_ctx* ctx);
+
 /* ---- synchronous host batches (bulk re-verify, torrent.rs:724-740) ----- */
 /* digests_out: n*20 bytes.  Pieces are pipelined through the slots, longest
  * first (ragged batches: DESIGN.md §6.4); outputs are always in the caller's

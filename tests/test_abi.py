@@ -34,6 +34,24 @@ def test_completion_layout():
     assert ctypes.sizeof(vx_config) == 24
 
 
+def test_stats_layout(tmp_path):
+    """vx_stats as ctypes (and INTEGRATION.md's VxStats, test_integration_doc)
+    has the C struct's size and offsets: C says so, compiled here."""
+    from vortex_amd._lib import VX_STATS_HIST, vx_stats
+
+    c = tmp_path / "s.c"
+    c.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "vx_hash.h"\nint main(void){printf("%zu %zu %zu %d\\n", '
+                 'sizeof(vx_stats), offsetof(vx_stats, submit_stall_ns), offsetof(vx_stats, batch_latency_hist), '
+                 'VX_STATS_HIST); return 0;}\n')
+    exe = tmp_path / "s"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(c), "-o",
+                    str(exe)], check=True)
+    size, stall, hist, nh = map(int, subprocess.run([str(exe)], capture_output=True, text=True,
+                                                     check=True).stdout.split())
+    assert (size, stall, hist, nh) == (ctypes.sizeof(vx_stats), vx_stats.submit_stall_ns.offset,
+                                       vx_stats.batch_latency_hist.offset, VX_STATS_HIST)
+
+
 def test_library_exports_declared_symbols(built):
     from vortex_amd import _lib
 

@@ -18,6 +18,7 @@ RUST_TO_C = {
     "u8": "uint8_t", "u32": "uint32_t", "u64": "uint64_t", "i32": "int32_t", "i64": "int64_t",
     "usize": "size_t", "c_int": "int", "c_char": "char", "c_void": "void", "f64": "double",
     "VxCtx": "vx_ctx", "VxConfig": "vx_config", "VxCompletion": "vx_completion", "VxPlan": "vx_plan",
+    "VxStats": "vx_stats",
 }
 
 
@@ -83,8 +84,7 @@ def c_structs():
                 continue
             fm = re.fullmatch(r"(\w+)\s+(\w+)(?:\[(\w+)\])?", line)
             ctype, fname, dim = fm.group(1), fm.group(2), fm.group(3)
-            if dim == "VX_DIGEST_LEN":
-                dim = "20"
+            dim = {"VX_DIGEST_LEN": "20", "VX_STATS_HIST": "24"}.get(dim, dim)
             fields.append((fname, ctype + (f"[{dim}]" if dim else "")))
         out[m.group(1)] = fields
     return out

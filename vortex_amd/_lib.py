@@ -38,7 +38,7 @@ EXPORTS = (
     "vx_sha1_device_uniform", "vx_sha1_device_ragged", "vx_sha1_device_ragged_hint", "vx_sort_order",
     "vx_synth_fill", "vx_sha1_device_uniform_variant", "vx_sha1_device_ragged_variant",
     "vx_tuning_chunk_rounds", "vx_tuning_gather_tiles", "vx_tuning_plan_ragged", "vx_tuning_chunk_schedule",
-    "vx_tuning_fail_submit_after", "vx_plan_verify",
+    "vx_tuning_fail_submit_after", "vx_plan_verify", "vx_get_stats", "vx_reset_stats",
 )
 
 
@@ -62,6 +62,16 @@ class vx_plan(ctypes.Structure):
     _fields_ = [("gpu_s", ctypes.c_double), ("gpu_chain_s", ctypes.c_double), ("gpu_transfer_s", ctypes.c_double),
                 ("cpu_s", ctypes.c_double), ("piece_latency_s", ctypes.c_double),
                 ("cpu_piece_latency_s", ctypes.c_double), ("use_gpu", ctypes.c_int32), ("_pad", ctypes.c_uint32)]
+
+
+VX_STATS_HIST = 24
+
+
+class vx_stats(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_uint64) for name in (
+        "pieces_completed", "pieces_mismatched", "bytes_completed", "batches", "chunk_rounds", "gather_tiles",
+        "staged_bytes", "io_errors", "submit_stall_ns", "batch_latency_count", "batch_latency_sum_us",
+        "batch_latency_max_us")] + [("batch_latency_hist", ctypes.c_uint64 * VX_STATS_HIST)]
 
 
 _lib = None
@@ -88,6 +98,8 @@ def _declare(L: ctypes.CDLL) -> None:
         "vx_poll": ([vp, c.POINTER(vx_completion), c.c_size_t], c.c_int64),
         "vx_drain": ([vp, c.c_uint32], c.c_int),
         "vx_pending": ([vp], c.c_uint64),
+        "vx_get_stats": ([vp, c.POINTER(vx_stats)], c.c_int),
+        "vx_reset_stats": ([vp], c.c_int),
         "vx_sha1_batch": ([vp, vp, vp, c.c_size_t, vp], c.c_int),
         "vx_verify_batch": ([vp, vp, vp, vp, c.c_size_t, vp, vp], c.c_int),
         "vx_verify_files": ([vp, vp, vp, c.c_size_t, c.c_uint32, vp, c.c_size_t, vp, c.c_uint32], c.c_int64),

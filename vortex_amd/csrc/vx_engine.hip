@@ -130,6 +130,7 @@ struct Slot {
     bool use_table = false;  // expected digests come from the device piece table
     enum State { FREE, FILLING, INFLIGHT } state = FREE;
     uint64_t seq = 0;
+    std::chrono::steady_clock::time_point t_open{};  // first piece queued (vx_stats batch latency)
 };
 
 }  // namespace
@@ -196,6 +197,7 @@ struct vx_ctx {
     // after this many more succeeds fails with VX_ENOMEM, the way a failed
     // pinned-stage allocation does; < 0 = off.
     int64_t fail_submit_after = -1;
+    vx_stats stats{};  // vx_get_stats (observability counters)
 };
 
 namespace {
@@ -482,6 +484,7 @@ int launch_slot_impl(vx_ctx* c, int si) {
         hipError_t e = vx::launch_gather(s.d_src, s.d_offsets, s.d_lens, s.d_tfirst, n, s.gtiles, s.d_arena, cs, grid);
         if (e != hipSuccess) return hip_fail(e, "gather launch");
         c->gather_tiles += s.gtiles;
+        c->stats.gather_tiles += s.gtiles;
     }
     if (s.use_table)
         VX_HIP(hipMemcpyAsync(s.d_pidx, s.h_pidx, (size_t)n * 4, hipMemcpyHostToDevice, cs));
@@ -514,16 +517,40 @@ int launch_slot_impl(vx_ctx* c, int si) {
     VX_HIP(hipEventRecord(s.done, s.stream));
     s.state = Slot::INFLIGHT;
     s.seq = c->seq++;
+    c->stats.batches++;
     return 0;
 }
 
+// Batch latency: first piece queued -> results harvested, into the log2
+// histogram of vx_stats.
+void record_batch_latency(vx_ctx* c, std::chrono::steady_clock::time_point t_open) {
+    const auto us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t_open);
+    const uint64_t v = (uint64_t)std::max<int64_t>(0, us.count());
+    vx_stats& st = c->stats;
+    st.batch_latency_count++;
+    st.batch_latency_sum_us += v;
+    st.batch_latency_max_us = std::max(st.batch_latency_max_us, v);
+    int k = 0;
+    while (k + 1 < VX_STATS_HIST && (v >> (k + 1)) != 0) ++k;
+    st.batch_latency_hist[k]++;
+}
+
 void harvest(vx_ctx* c, Slot& s) {
+    uint64_t bytes = 0, bad = 0;
     for (uint32_t i = 0; i < s.n; ++i) {
         vx_completion r{};
         r.tag = s.tags[i];
         r.matched = s.has_expected ? s.h_matched[i] : 0;
         std::memcpy(r.digest, s.h_digests + (size_t)i * 20, 20);
         c->done.push_back(r);
+        bytes += s.h_lens[i];
+        bad += s.has_expected && !r.matched;
+    }
+    if (s.n) {
+        c->stats.pieces_completed += s.n;
+        c->stats.pieces_mismatched += bad;
+        c->stats.bytes_completed += bytes;
+        record_batch_latency(c, s.t_open);
     }
     reset_fill(s);
     s.state = Slot::FREE;
@@ -569,7 +596,10 @@ int acquire_filling(vx_ctx* c) {
                 return i;
             }
         }
+        const auto t0 = std::chrono::steady_clock::now();
         int rc = reap(c, /*block_oldest=*/true);
+        c->stats.submit_stall_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                        std::chrono::steady_clock::now() - t0).count();
         if (rc) return rc;
     }
 }
@@ -600,6 +630,7 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
     const uint32_t i = s->n;
     const uint8_t* dev = nullptr;
     s->h_src[i] = 0;
+    if (i == 0) s->t_open = std::chrono::steady_clock::now();
     if (len && c->gather && (reinterpret_cast<uintptr_t>(data) & 15) == 0 && is_registered(c, data, len, &dev)) {
         // Registered, 16-byte aligned: the launch's gather kernel pulls it
         // through the range's device mapping.
@@ -616,6 +647,7 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
                 s->druns.push_back(DirectRun{data, off, off + len});
         } else {
             if (int rc = ensure_stage(*s)) return rc;
+            c->stats.staged_bytes += len;
             if (c->bulk) {  // a host batch: copied in parallel at launch (stage_copies)
                 s->staged.push_back(StageCopy{data, off, len});
                 s->staged_bytes += len;
@@ -1005,6 +1037,7 @@ int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl,
             reset_fill(s);
             if ((rc = ensure_stage(s))) break;
             s.state = Slot::FILLING;  // reserved until launched
+            s.t_open = std::chrono::steady_clock::now();
             uint64_t cap = filled < ramp ? std::max<uint64_t>(1, cap_full >> (ramp - filled)) : cap_full;
             const uint64_t rem = end - next, smallest = std::max<uint64_t>(1, cap_full >> ramp);
             if (ramp > 0 && rem <= cap && rem > smallest) cap = std::max(smallest, (rem + 1) / 2);
@@ -1055,6 +1088,7 @@ int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl,
 struct ChunkPipe {
     vx_ctx* c;
     uint64_t cnt = 0;
+    uint64_t bytes = 0;  // the call's piece bytes (vx_stats)
     uint32_t* d_states = nullptr;
     uint8_t *d_exp = nullptr, *d_dig = nullptr, *d_match = nullptr;
     hipEvent_t prev_kernel = nullptr;
@@ -1159,6 +1193,7 @@ struct ChunkPipe {
             rc = fail(VX_EDEVICE, "chunk round: event record failed");
         have_prev = true;
         c->chunk_rounds++;
+        c->stats.chunk_rounds++;
         s.state = Slot::INFLIGHT;
         s.seq = c->seq++;
         s.n = 0;  // nothing to harvest: outputs live in the call's device rows
@@ -1178,6 +1213,12 @@ struct ChunkPipe {
             rc = fail(VX_EDEVICE, "verdict D2H failed");
         if (!rc && digests_out && hipMemcpy(digests_out, d_dig, cnt * 20, hipMemcpyDeviceToHost) != hipSuccess)
             rc = fail(VX_EDEVICE, "digest D2H failed");
+        if (!rc) {
+            c->stats.pieces_completed += cnt;
+            c->stats.bytes_completed += bytes;
+            if (matched_out && d_match)
+                for (uint64_t i = 0; i < cnt; ++i) c->stats.pieces_mismatched += matched_out[i] == 0;
+        }
         for (auto& s : c->slots)
             if (s.state == Slot::INFLIGHT) {
                 (void)hipEventSynchronize(s.done);
@@ -1245,6 +1286,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     const uint64_t cnt = end - first;
     ChunkPipe cp(c);
     int rc = cp.open(cnt, fv.expected + 20 * first, "vx_verify_files");
+    cp.bytes = cnt * (uint64_t)pl - (end == n ? (uint64_t)pl - last_len : 0);
     // windows of W pieces; each window runs its rounds in order
     const Slot& s0 = c->slots[0];
     const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>(s0.cap, s0.arena_cap / C));
@@ -1406,6 +1448,7 @@ int batch_chunked(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, c
     const uint8_t* base = ptrs[0];
     ChunkPipe cp(c);
     int rc = cp.open(n, expected, "batch");
+    for (size_t i = 0; i < n; ++i) cp.bytes += lens[i];
     const Slot& s0 = c->slots[0];
     const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>(s0.cap, s0.arena_cap / C));
     const uint64_t rounds = (L + C - 1) / C;
@@ -1476,6 +1519,7 @@ int batch_chunked_gather(vx_ctx* c, const uint32_t* lens, const uint8_t* expecte
     const uint64_t C = c->batch_chunk;
     ChunkPipe cp(c);
     int rc = cp.open(n, expected, "batch");
+    for (size_t i = 0; i < n; ++i) cp.bytes += lens[i];
     const Slot& s0 = c->slots[0];
     const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>(s0.cap, s0.arena_cap / C));
     // Windows take the pieces longest first (stable, so equal lengths keep the
@@ -1499,6 +1543,7 @@ int batch_chunked_gather(vx_ctx* c, const uint32_t* lens, const uint8_t* expecte
                                              c->gather_grid);
             if (e != hipSuccess) return hip_fail(e, "batch: gather launch");
             c->gather_tiles += tiles;
+            c->stats.gather_tiles += tiles;
             return 0;
         };
     };
@@ -1750,6 +1795,7 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
     if (rc) return rc;
     int64_t nbad = 0;
     for (uint8_t x : bad) nbad += x;
+    c->stats.io_errors += (uint64_t)nbad;
     return nbad;
 }
 
@@ -1902,6 +1948,18 @@ int vx_plan_verify(uint64_t n_pieces, uint32_t piece_length, uint64_t total_leng
     out->piece_latency_s = out->gpu_chain_s + kBatchLatency;
     out->cpu_piece_latency_s = L / rate;
     out->use_gpu = out->gpu_s * kMargin < out->cpu_s ? 1 : 0;
+    return 0;
+}
+
+int vx_get_stats(const vx_ctx* c, vx_stats* out) {
+    if (!c || !out) return fail(VX_EINVAL, "vx_get_stats: NULL argument");
+    *out = c->stats;
+    return 0;
+}
+
+int vx_reset_stats(vx_ctx* c) {
+    if (!c) return fail(VX_EINVAL, "vx_reset_stats: NULL context");
+    c->stats = vx_stats{};
     return 0;
 }
 

@@ -33,7 +33,7 @@ from dataclasses import dataclass
 from typing import Any, Iterable, Optional, Sequence
 
 from . import _lib
-from ._lib import check, lib, vx_completion, vx_config
+from ._lib import check, lib, vx_completion, vx_config, vx_stats
 
 
 @dataclass
@@ -198,6 +198,19 @@ class HashPool:
     @property
     def pending(self) -> int:
         return int(lib().vx_pending(self._h))
+
+    # -- observability (vx_get_stats) -------------------------------------------
+    def stats(self) -> dict:
+        """The engine's counters (include/vx_hash.h vx_stats) as a dict; the
+        latency histogram is a list of VX_STATS_HIST log2 buckets in us."""
+        st = vx_stats()
+        check(lib().vx_get_stats(self._h, ctypes.byref(st)), "vx_get_stats")
+        out = {name: int(getattr(st, name)) for name, _ in vx_stats._fields_ if name != "batch_latency_hist"}
+        out["batch_latency_hist"] = [int(x) for x in st.batch_latency_hist]
+        return out
+
+    def reset_stats(self) -> None:
+        check(lib().vx_reset_stats(self._h), "vx_reset_stats")
 
     # -- bulk verify -----------------------------------------------------------
     def sha1_batch(self, pieces: Sequence) -> list[bytes]:
