@@ -85,14 +85,15 @@ def test_stats_submit_stall(built, gpu):
 
     plen = 1 << 20
     body = bytearray(oracle.gen_piece(3, 0, plen))
+    good = hashlib.sha1(body).digest()
     with HashPool(plen, slots=2, batch_pieces=4) as pool:
         for i in range(12):
-            pool.spawn(i, 0, body, plen)
+            pool.spawn(i, 0, body, plen, good)
         pool.drain()
         assert len(pool.try_iter()) == 12
         st = pool.stats()
         assert st["submit_stall_ns"] > 0
-        assert st["pieces_completed"] == 12 and st["pieces_mismatched"] == 0  # no expected digests
+        assert st["pieces_completed"] == 12 and st["pieces_mismatched"] == 0
         _check_latency(st)
 
 
