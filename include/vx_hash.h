@@ -100,7 +100,9 @@ void vx_config_default(vx_config* cfg, uint32_t max_piece_len);
  *      the rayon scope it feeds (torrent.rs:319-320, 333; event_loop.rs:385) */
 int vx_create(const vx_config* cfg, vx_ctx** out);
 /* Drains all in-flight work first (the reference's scope joins every spawned
- * hash before EventLoop::run returns, event_loop.rs:385-602), then frees. */
+ * hash before EventLoop::run returns, event_loop.rs:385-602), then frees.
+ * On a failed context it waits for the device to stop (every stream) before
+ * unregistering host buffers, so borrowed buffers are free once it returns. */
 int vx_destroy(vx_ctx* ctx);
 
 /* Pin and device-map a host range (e.g. a BufferPool's AnonymousMmap,
@@ -135,7 +137,11 @@ int vx_flush(vx_ctx* ctx);
 /* Replaces `downloaded_piece_rc.try_recv()` (torrent.rs:418): non-blocking,
  * returns how many completions were written to out[0..max).  Order is the
  * order batches finish, which like the reference is not submission order.
- * Returns a negative VX_E* if a batch failed on the device. */
+ * Returns a negative VX_E* if a batch failed on the device.  After such a
+ * failure the context is dead (every call returns the error), but vx_poll
+ * still hands out the results of batches that did finish, and returns the
+ * error only once none is left: the tags never returned are the pieces to
+ * hash elsewhere (INTEGRATION.md "Device failure"). */
 int64_t vx_poll(vx_ctx* ctx, vx_completion* out, size_t max);
 /* Flush and block until every submitted piece has completed (results stay
  * queued for vx_poll).  timeout_ms = 0 waits forever. */

@@ -32,6 +32,10 @@ uint64_t vx_tuning_gather_tiles(const struct vx_ctx* ctx);
  * inside a host batch), the next one fails with VX_ENOMEM without latching
  * the context, as a failed pinned-stage allocation does.  k < 0 turns it off. */
 void vx_tuning_fail_submit_after(struct vx_ctx* ctx, int64_t k);
+/* Fault injection for tests: after k more successful batch launches, the next
+ * launch fails as a device error does (VX_EDEVICE, the context turns sticky):
+ * the recovery path of INTEGRATION.md "Device failure".  k < 0 turns it off. */
+void vx_tuning_fail_launch_after(struct vx_ctx* ctx, int64_t k);
 /* The kernel vx_sha1_device_ragged_hint runs for a batch of n pieces whose
  * longest is max_len bytes, total_len bytes in all: 1 = lane, 2 = split,
  * 5 = split with one pair per CU (host-only). */

@@ -9,6 +9,9 @@
   launch by up to 16 threads (stage_copies); slots of 64 MiB and more split
   the copy, and the result must still be bit-exact.
 * register_buffer refuses read-only objects and unregisters by object.
+* A device failure in mid-stream (injected launch failure) leaves a dead
+  context that still returns every finished result, names exactly the pieces
+  to re-hash, and is destroyed cleanly.
 """
 import hashlib
 import mmap
@@ -147,3 +150,54 @@ def test_ragged_layout_validation(built, gpu):
         run([0, 16], [1, 1], order=[0])
     with pytest.raises(ValueError):
         vdev.sha1_uniform(data, 2, 2049, stride=2064)  # 2064 + 2049 > 4096
+
+
+def test_device_failure_recovery(built, gpu):
+    """A device failure in mid-stream (injected: the 3rd launch fails as a
+    device error would, vx_tuning_fail_launch_after) turns the context
+    sticky.  The caller's recovery (INTEGRATION.md "Device failure"): every
+    result the device did produce still comes back from vx_poll, then the
+    error; the pieces whose result never came are exactly the ones to hash on
+    vortex's own pool; destroying the context waits for the device to stop
+    reading registered buffers, and a new context on the same GPU works."""
+    import time
+
+    from vortex_amd._lib import VX_EDEVICE, VxError, lib
+    from vortex_amd.hash_pool import HashPool
+
+    plen, n = 65536 + 32, 48
+    pinned = mmap.mmap(-1, n * plen)
+    bodies = [oracle.gen_piece(0xDEAD, i, plen) for i in range(n)]
+    for i, b in enumerate(bodies):
+        pinned[i * plen:(i + 1) * plen] = b
+    digests = [hashlib.sha1(b).digest() for b in bodies]
+    pool = HashPool(plen, slots=3, batch_pieces=8)
+    pool.register_buffer(pinned)
+    lib().vx_tuning_fail_launch_after(pool._h, 2)
+    results, refused = {}, None
+    for i in range(n):
+        try:
+            pool.spawn(i, i, memoryview(pinned)[i * plen:(i + 1) * plen], plen, digests[i])
+        except VxError as e:
+            assert e.code == VX_EDEVICE
+            refused = i
+            break
+    assert refused == 23  # the third batch fills at the 24th submit and fails to launch
+    time.sleep(0.5)  # the two launched batches finish
+    for r in pool.try_iter():
+        assert r.hash_matched and r.digest == digests[r.index]
+        results[r.index] = True
+    with pytest.raises(VxError) as ei:
+        pool.try_iter()
+    assert ei.value.code == VX_EDEVICE
+    assert sorted(results) == list(range(16))
+    lost = pool.take_unfinished()
+    assert sorted(idx for idx, _, _ in lost) == list(range(16, 23))
+    for idx, _, buf in lost + [(refused, refused, memoryview(pinned)[refused * plen:(refused + 1) * plen])]:
+        assert hashlib.sha1(bytes(buf[:plen])).digest() == digests[idx]  # the caller's pool takes over
+    pool.close()  # waits for the streams, then unregisters and frees
+    with HashPool(plen, slots=2, batch_pieces=8) as fresh:
+        for i in range(10):
+            fresh.spawn(i, i, bytearray(bodies[i]), plen, digests[i])
+        fresh.drain()
+        assert sorted(r.index for r in fresh.try_iter() if r.hash_matched) == list(range(10))

@@ -197,6 +197,9 @@ struct vx_ctx {
     // after this many more succeeds fails with VX_ENOMEM, the way a failed
     // pinned-stage allocation does; < 0 = off.
     int64_t fail_submit_after = -1;
+    // vx_tuning_fail_launch_after: the launch after this many more fails as a
+    // device error would, turning the context sticky; < 0 = off.
+    int64_t fail_launch_after = -1;
     vx_stats stats{};  // vx_get_stats (observability counters)
 };
 
@@ -445,6 +448,8 @@ int warm_slots(vx_ctx* c) {
 // A failed launch leaves a slot half-enqueued: the context turns sticky and
 // every later call reports the error (vx_destroy still cleans up).
 int launch_slot(vx_ctx* c, int si) {
+    if (c->fail_launch_after >= 0 && c->fail_launch_after-- == 0)
+        return c->sticky = fail(VX_EDEVICE, "launch: injected device failure (vx_tuning_fail_launch_after)");
     const int rc = launch_slot_impl(c, si);
     if (rc) c->sticky = rc;
     return rc;
@@ -786,6 +791,13 @@ int vx_destroy(vx_ctx* c) {
     if (!c) return 0;
     int rc = c->sticky ? 0 : vx_drain(c, 0);
     set_device(c);
+    // A failed (sticky) context skipped the drain: batches may still be
+    // running, and a gather kernel may still read registered host memory.
+    // Wait for every stream before unregistering anything, so the caller can
+    // return in-flight buffers to its pool as soon as this call returns.
+    for (auto& s : c->slots)
+        if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     for (auto& r : c->registered) (void)hipHostUnregister(reinterpret_cast<void*>(r.first));
     for (auto& s : c->slots) free_slot_mem(s);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
@@ -885,12 +897,21 @@ int vx_flush(vx_ctx* c) {
 
 int64_t vx_poll(vx_ctx* c, vx_completion* out, size_t max) {
     if (!c || (!out && max)) return fail(VX_EINVAL, "vx_poll: bad argument");
-    if (c->sticky) return c->sticky;
     int rc = set_device(c);
     if (rc) return rc;
-    rc = reap(c, false);
-    if (rc) return rc;
-    if (c->flush_pending && c->filling >= 0 && may_launch_now(c) && (rc = launch_slot(c, c->filling))) return rc;
+    if (c->sticky) {
+        // Failed context: hand out every result the device did produce (batches
+        // that finished, harvested now or earlier), then the error.  The tags
+        // never returned are the pieces to re-hash elsewhere.
+        const int sticky = c->sticky;
+        (void)reap(c, false);
+        c->sticky = sticky;
+        if (c->done.empty()) return sticky;
+    } else {
+        rc = reap(c, false);
+        if (rc) return rc;
+        if (c->flush_pending && c->filling >= 0 && may_launch_now(c) && (rc = launch_slot(c, c->filling))) return rc;
+    }
     size_t k = 0;
     while (k < max && !c->done.empty()) {
         out[k++] = c->done.front();
@@ -1967,6 +1988,9 @@ uint64_t vx_tuning_chunk_rounds(const vx_ctx* c) { return c ? c->chunk_rounds : 
 uint64_t vx_tuning_gather_tiles(const vx_ctx* c) { return c ? c->gather_tiles : 0; }
 void vx_tuning_fail_submit_after(vx_ctx* c, int64_t k) {
     if (c) c->fail_submit_after = k < 0 ? -1 : k;
+}
+void vx_tuning_fail_launch_after(vx_ctx* c, int64_t k) {
+    if (c) c->fail_launch_after = k < 0 ? -1 : k;
 }
 size_t vx_tuning_chunk_schedule(uint64_t L, uint64_t C, int head, int tail, uint64_t* out, size_t max) {
     if (C < 4 || C % 4) return 0;

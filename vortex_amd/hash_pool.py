@@ -190,6 +190,16 @@ class HashPool:
             if len(got) < len(self._cbuf):
                 return out
 
+    def take_unfinished(self) -> list[tuple[int, int, Any]]:
+        """After a device error (a VxError from spawn / try_recv / try_iter):
+        (index, conn_id, buffer) of every submitted piece whose result never
+        came back, for the caller to hash on its own pool (INTEGRATION.md
+        "Device failure").  Close the pool before reusing those buffers: that
+        waits for the device to stop reading them."""
+        out = [(index, conn_id, buffer) for index, conn_id, buffer, _keep in self._inflight.values()]
+        self._inflight.clear()
+        return out
+
     def drain(self, timeout_ms: int = 0) -> None:
         """Flush and wait for all in-flight pieces (the scope join of
         event_loop.rs:385-602); results stay queued for try_recv."""
