@@ -443,9 +443,12 @@ def roofline(n: int, plen: int, kern_ms: float, achieved: float, workload: str) 
                          "achieved_Gwaveops_per_s": round(wave_ops / 1e9, 1),
                          "ceiling_Gwaveops_per_s": [stream["lo"], stream["hi"]],
                          "clock_GHz": stream["clock_GHz"],
-                         "frac": [round(wave_ops / 1e9 / stream["hi"], 4), round(wave_ops / 1e9 / stream["lo"], 4)],
+                         "frac_vs_fast_clock": round(wave_ops / 1e9 / stream["hi"], 4),
+                         "frac_vs_slow_clock": round(wave_ops / 1e9 / stream["lo"], 4),
                          "source": "profiles/r02/valu/energy_probe_run*.json: SHA-1 round ops, 1 wave on each of "
-                                   "the 1,024 SIMDs, ~1.5-2 s; the range is the chip's two clock states"},
+                                   "the 1,024 SIMDs, ~1.5-2 s; the two ceilings are the two clock states the chip "
+                                   "ran such streams at. A frac_vs_slow_clock near or above 1 means the kernel ran "
+                                   "at (or above) the slow state's clock and is at that clock's ceiling"},
                      "simd32_vop2_only": {"peak_Tops": round(peak(2.0) / 1e12, 2), "frac": round(ops / peak(2.0), 4)},
                      "pmc": pmc,
                      "note": "65,536 pieces = exactly one wave per SIMD. Every SHA-1 op but the schedule's "
