@@ -299,6 +299,9 @@ def ragged_leg(dev, stream, steps: int = 5):
     per_block_us = ms * 1e3 / blocks
     floor_valu_us = 405 * 4 / 2.4e9 * 1e6     # rounds only: 405 VALU at one wave's 4-cycle issue, 2.4 GHz
     floor_inst_us = 425 * 4 / 2.4e9 * 1e6     # + the consumer's 20 ds_read_b128 issue slots
+    # the generated consumer alone (no producer, no barriers) with its 20-read burst per block:
+    # 1,775 cycles (tools/native/pair_probe.hip no_barriers_idle_producer, profiles/r02/consumer_asm/)
+    floor_reads_us = 1775.4 / 2.4e9 * 1e6
     del data, d_off, d_len, order, dig, expected, matched
     torch.cuda.empty_cache()
     return {"value": round(total / (ms * 1e-3) / GiB, 2), "unit": "GiB/s", "kernel_ms_median": round(ms, 3),
@@ -309,8 +312,12 @@ def ragged_leg(dev, stream, steps: int = 5):
                       "floor_405_valu_us": round(floor_valu_us, 4), "floor_425_inst_us": round(floor_inst_us, 4),
                       "frac_of_valu_floor": round(floor_valu_us / per_block_us, 4),
                       "frac_of_inst_floor": round(floor_inst_us / per_block_us, 4),
+                      "floor_consumer_with_reads_us": round(floor_reads_us, 4),
+                      "frac_of_consumer_with_reads": round(floor_reads_us / per_block_us, 4),
                       "note": "one 4 MiB piece is a chain of 65,537 dependent compressions in one lane; "
-                              "floors at one wave's 4-cycle issue and nominal 2.4 GHz (DESIGN.md §3.2)"},
+                              "floors at nominal 2.4 GHz: 405 VALU / 425 instructions at one wave's 4-cycle "
+                              "issue, and the measured consumer stream with its LDS reads (the pair's real "
+                              "floor: barriers and the producer add < 1 %, DESIGN.md §3.2.1)"},
             "sample": "config 3: 262,144 x 16 KiB + 16,384 x 256 KiB + 4,096 x 1 MiB + 1,024 x 4 MiB, shuffled, "
                       "device-resident, verify vs expected table, median of %d launches" % steps}
 

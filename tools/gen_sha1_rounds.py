@@ -418,6 +418,8 @@ def main():
     ap.add_argument("--consumer6", help="write the 6-slot, barrier-per-pair consumer header (probe only: "
                                            "no faster in the kernels, DESIGN.md §3.2.1)")
     ap.add_argument("--consumerf", help="write the flag-handshake consumer header (consumer_flags_asm)")
+    ap.add_argument("--consumer-nobarrier", help="probe only: the 3-slot consumer with every s_barrier replaced "
+                                                 "by s_nop 0 (what the barrier costs; no synchronisation)")
     ap.add_argument("--mode", default="burst", choices=["refill", "burst", "burst2", "spread"],
                     help="ring-read placement (burst: the kernel's; A/B in DESIGN.md §3.2)")
     a = ap.parse_args()
@@ -433,6 +435,14 @@ def main():
         write_consumer_header(a.consumer6, a.mode, slots=6)
     if a.consumerf:
         write_consumerf_header(a.consumerf)
+    if a.consumer_nobarrier:
+        with open(a.consumer_nobarrier, "w") as f:
+            f.write("// GENERATED by tools/gen_sha1_rounds.py --consumer-nobarrier; do not edit.\n"
+                    "// Probe only: the consumer with s_barrier -> s_nop 0 (no synchronisation).\n#pragma once\n\n")
+            f.write("#define VX_CONSUMERNB_ASM \\\n")
+            for line in consumer_asm(False, "burst").replace("s_barrier", "s_nop 0").splitlines():
+                f.write(f'    "{line}\\n" \\\n')
+            f.write('    ""\n')
     if a.header:
         body = emit(ins, final, R.h)
         regs = sorted({r for r in R.h + R.w + R.a + R.c + R.x + R.f + [R.r]}, key=lambda r: int(r[1:]))

@@ -15,6 +15,18 @@
 //   7  as 2 with no barriers: an LDS flag handshake (producer count / consumer
 //      count, tools/gen_sha1_rounds.py consumer_flags_asm), bounded waits
 //   8  as 7 with the producer passing the flags only (no LDS writes, no VALU)
+//   9  as 2 with the producer's 210 VALU all VOP2 (v_add_u32_e32): does the
+//      interference follow the producer's instruction count or its VALU cycles?
+//   10 as 2 with half the producer VALU (105 VOP3)
+//   11 as 1 (LDS writes, no VALU) with the 6-slot ring: one barrier per 2 blocks
+//   12 the real producer's VALU: 16 v_perm + 64 x (xor3, xor, rotl1) as VOP3
+//      (bitop3 0x96, bitop3 0x3c, alignbit), 3-slot ring
+//   13 as 12 with the 6-slot ring
+//   14 as 12 with the 2-input xor as VOP2 v_xor_b32_e32 (144 VOP3 + 64 VOP2)
+//   15 as 14 with the 6-slot ring
+//   16 no synchronisation: the consumer with s_barrier -> s_nop 0 and an idle
+//      producer wave (what the barriers cost; the consumer reads stale slots)
+//   17 as 16 with the producer wave running the real producer's VALU unsynchronised
 // The consumer stamps s_memtime around its whole loop; prints cycles per
 // block (median over pairs) and the wall ns per block.  No HBM traffic.
 #include <hip/hip_runtime.h>
@@ -26,6 +38,7 @@
 #include "../../vortex_amd/csrc/sha1_consumer_asm.inc"
 #include "sha1_consumer6_asm.inc"  // python tools/gen_sha1_rounds.py --consumer6 tools/native/sha1_consumer6_asm.inc
 #include "sha1_consumerf_asm.inc"  // python tools/gen_sha1_rounds.py --consumerf tools/native/sha1_consumerf_asm.inc
+#include "sha1_consumernb_asm.inc"  // python tools/gen_sha1_rounds.py --consumer-nobarrier tools/native/sha1_consumernb_asm.inc
 
 template <int S>
 struct Ring {
@@ -34,16 +47,17 @@ struct Ring {
 
 template <int P>
 __global__ __launch_bounds__(128) void pair(uint32_t nb, uint32_t* out, unsigned long long* cyc) {
-    constexpr int S = P == 6 ? 6 : 3;  // 6: barrier per pair of blocks (VX_CONSUMER6_ASM)
+    constexpr int S = (P == 6 || P == 11 || P == 13 || P == 15) ? 6 : 3;  // 6: barrier per 2 blocks (VX_CONSUMER6_ASM)
     __shared__ Ring<S> lds;
-    __shared__ uint32_t flags[4];  // P >= 7: {prod, cons, consumer gave up, producer gave up}
+    __shared__ uint32_t flags[4];  // P = 7, 8: {prod, cons, consumer gave up, producer gave up}
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (P >= 7) {
+    constexpr bool F = P == 7 || P == 8;  // flag handshake instead of barriers
+    if (F) {
         if (threadIdx.x < 4) flags[threadIdx.x] = 0;
         __syncthreads();
     }
-    if (wave == 1 && P >= 7) {  // flag-handshake producer
+    if (wave == 1 && F) {  // flag-handshake producer
         uint32_t x = lane * 0x9E3779B9u, y = 0x12345u + lane;
         for (uint32_t b = 0; b < nb; ++b) {
             if (P == 7) {
@@ -71,16 +85,66 @@ __global__ __launch_bounds__(128) void pair(uint32_t nb, uint32_t* out, unsigned
         out[blockIdx.x * 64 + lane] = x ^ y;
         return;
     }
+    if (wave == 1 && P >= 16) {  // unsynchronised producer
+        if (P == 17) {
+            uint32_t w[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) w[k] = lane * 0x9E3779B9u + k;
+            for (uint32_t b = 0; b < nb; ++b) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_perm(w[k], w[k] + b, 0x00010203u);
+#pragma unroll
+                for (int t = 16; t < 80; ++t) {
+                    uint32_t v = __builtin_amdgcn_bitop3_b32(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15], 0x96);
+                    v = __builtin_amdgcn_bitop3_b32(v, w[t & 15], w[t & 15], 0x3C);
+                    w[t & 15] = __builtin_amdgcn_alignbit(v, v, 31);
+                }
+#pragma unroll
+                for (int q = 0; q < 20; ++q)
+                    lds.w[b % S][q][lane] = make_uint4(w[(4 * q) & 15], w[(4 * q + 1) & 15], w[(4 * q + 2) & 15],
+                                                       w[(4 * q + 3) & 15]);
+            }
+            out[blockIdx.x * 64 + lane] = w[0];
+        }
+        return;
+    }
     if (wave == 1) {  // producer
         uint32_t x = lane * 0x9E3779B9u, y = 0x12345u + lane;
+        uint32_t w[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = x + k * y;
         for (uint32_t b = 0; b < nb; ++b) {
-            if (P == 4) {
+            if (P >= 12) {  // the real producer's schedule work per block
+#pragma unroll
+                for (int k = 0; k < 16; ++k) w[k] = __builtin_amdgcn_perm(w[k], w[k] + b, 0x00010203u);
+#pragma unroll
+                for (int t = 16; t < 80; ++t) {
+                    uint32_t v = __builtin_amdgcn_bitop3_b32(w[(t - 3) & 15], w[(t - 8) & 15], w[(t - 14) & 15], 0x96);
+                    v = (P >= 14) ? (v ^ w[t & 15]) : __builtin_amdgcn_bitop3_b32(v, w[t & 15], w[t & 15], 0x3C);
+                    w[t & 15] = __builtin_amdgcn_alignbit(v, v, 31);
+                }
+                x = w[0];
+                y = w[5];
+            } else if (P == 4) {
                 // the same 210 VALU as a short rolled loop (no instruction-fetch stream)
                 for (int i = 0; i < 70; ++i) {
                     x = __builtin_amdgcn_alignbit(x, x, 31) ^ y;
                     y = __builtin_amdgcn_bitop3_b32(x, y, 0x5a5a5a5au, 0x96);
                     x = x + y;
                     asm volatile("" : "+v"(x), "+v"(y));
+                }
+            } else if (P == 9) {
+#pragma unroll
+                for (int i = 0; i < 105; ++i) {  // 210 VOP2 adds
+                    x = x + y;
+                    y = y + x;
+                }
+            } else if (P == 10) {
+#pragma unroll
+                for (int i = 0; i < 35; ++i) {  // 105 VALU
+                    x = __builtin_amdgcn_alignbit(x, x, 31) ^ y;
+                    y = __builtin_amdgcn_bitop3_b32(x, y, 0x5a5a5a5au, 0x96);
+                    x = x + y;
                 }
             } else if (P >= 2) {
 #pragma unroll
@@ -90,7 +154,12 @@ __global__ __launch_bounds__(128) void pair(uint32_t nb, uint32_t* out, unsigned
                     x = x + y;
                 }
             }
-            if (P >= 1) {
+            if (P >= 12) {
+#pragma unroll
+                for (int q = 0; q < 20; ++q)
+                    lds.w[b % S][q][lane] = make_uint4(w[(4 * q) & 15], w[(4 * q + 1) & 15], w[(4 * q + 2) & 15],
+                                                       w[(4 * q + 3) & 15]);
+            } else if (P >= 1) {
 #pragma unroll
                 for (int q = 0; q < 20; ++q) lds.w[b % S][q][lane] = make_uint4(x + q, y, x ^ q, b);
             }
@@ -110,7 +179,12 @@ __global__ __launch_bounds__(128) void pair(uint32_t nb, uint32_t* out, unsigned
     const uint32_t zero = 0;
     const uint32_t faddr = (uint32_t)(uintptr_t)&flags[0];
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    if (P >= 7)
+    if (P >= 16)
+        asm volatile(VX_CONSUMERNB_ASM
+                     : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3), "+v"(h4)
+                     : "v"(addr), "s"(nb), "s"(nb), "v"(zero)
+                     : VX_CONSUMER_ASM_CLOBBERS, "memory");
+    else if (F)
         asm volatile(VX_CONSUMERF_ASM
                      : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3), "+v"(h4)
                      : "v"(addr), "s"(nb), "s"(nb), "v"(zero), "v"(faddr)
@@ -127,7 +201,7 @@ __global__ __launch_bounds__(128) void pair(uint32_t nb, uint32_t* out, unsigned
                      : VX_CONSUMER_ASM_CLOBBERS, "memory");
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     out[blockIdx.x * 64 + lane] = h0 ^ h1 ^ h2 ^ h3 ^ h4;
-    if (lane == 0) cyc[blockIdx.x] = (P >= 7 && (flags[2] | flags[3])) ? ~0ull : t1 - t0;
+    if (lane == 0) cyc[blockIdx.x] = (F && (flags[2] | flags[3])) ? ~0ull : t1 - t0;
 }
 
 template <int P>
@@ -166,6 +240,17 @@ int main() {
     run<8>("flags_only", 64, d, dc, true);
     run<7>("flags_lds_writes_valu", 64, d, dc, true);
     run<7>("flags_lds_writes_valu_2_pairs_per_cu", 512, d, dc, true);
+    run<9>("lds_writes_valu_vop2_adds", 64, d, dc, true);
+    run<10>("lds_writes_half_valu", 64, d, dc, true);
+    run<11>("lds_writes_6slots", 64, d, dc, true);
+    run<12>("real_producer_vop3_xor", 64, d, dc, true);
+    run<13>("real_producer_vop3_xor_6slots", 64, d, dc, true);
+    run<14>("real_producer_vop2_xor", 64, d, dc, true);
+    run<15>("real_producer_vop2_xor_6slots", 64, d, dc, true);
+    run<12>("real_producer_vop3_xor_2_pairs_per_cu", 512, d, dc, true);
+    run<14>("real_producer_vop2_xor_2_pairs_per_cu", 512, d, dc, true);
+    run<16>("no_barriers_idle_producer", 64, d, dc, true);
+    run<17>("no_barriers_real_producer_unsynced", 64, d, dc, true);
     std::printf("}\n");
     return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
