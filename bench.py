@@ -198,6 +198,7 @@ def e2e_batch(plen: int, n: int = 8192):
         _register_all(pool, bufs)
         t_reg = time.perf_counter() - t0
         check(lib().vx_verify_batch(pool._h, ptrs, lens, exp, 256, matched, digests), "warm")
+        pool.reset_stats()
         runs = []
         for _ in range(3):
             ctypes.memset(matched, 0, n)
@@ -205,12 +206,14 @@ def e2e_batch(plen: int, n: int = 8192):
             check(lib().vx_verify_batch(pool._h, ptrs, lens, exp, n, matched, digests), "vx_verify_batch")
             runs.append(time.perf_counter() - t0)
             assert matched.raw[:n] == b"\x01" * n
+        st = pool.stats()
         _unregister_all(pool, bufs)
     del ptrs, addrs
     el = sorted(runs)[1]
     return {"value": round(n * plen / el / GiB, 3), "unit": "GiB/s",
             "runs_GiBps": [round(n * plen / r / GiB, 2) for r in runs],
             "register_s": round(t_reg, 3),
+            "engine": {k: st[k] for k in ("pieces_completed", "batches", "chunk_rounds", "gather_tiles", "staged_bytes")},
             "sample": f"{n} x {plen // 1024} KiB, one registered mmap per piece (buf_pool.rs:92-98), "
                       f"vx_verify_batch (gather kernel + hash + D2H), median of 3 calls, {el * 1e3:.1f} ms"}
 
@@ -233,6 +236,7 @@ def e2e_async(plen: int, n: int = 8192):
         return {"error": f"async_probe rc={p.returncode}: {p.stderr[-300:]}"}
     d = json.loads(p.stdout.strip().splitlines()[-1])
     return {"value": d["GiBps"], "unit": "GiB/s", "mismatched": d["mismatched"], "polled": d["polled"],
+            "engine": d.get("engine"),
             "sample": f"{d['pieces']} x {plen // 1024} KiB from {n} separately registered mmaps, shuffled, "
                       f"vx_submit + vx_flush every 64 + vx_poll (tools/native/async_probe)"}
 
@@ -354,6 +358,7 @@ def reverify_leg(reps: int = 3):
         with HashPool(pl, slots=4, slot_bytes=512 << 20, batch_pieces=4096) as pool:
             got, bad = pool.verify_files([path], [total], pl, exp, io_threads=threads)  # warm (stages, rows)
             assert all(got) and bad == 0
+            pool.reset_stats()
             for _ in range(reps):
                 t0 = time.perf_counter()
                 got, bad = pool.verify_files([path], [total], pl, exp, io_threads=threads)
@@ -363,6 +368,7 @@ def reverify_leg(reps: int = 3):
                 cpu = oracle.pool_verify_files([path], [total], pl, exp, threads=threads)
                 cpu_t.append(time.perf_counter() - t0)
                 assert all(cpu)
+            st = pool.stats()
     finally:
         if os.path.exists(path):
             os.unlink(path)
@@ -371,6 +377,8 @@ def reverify_leg(reps: int = 3):
             "cpu_pool": {"value": round(total / c / GiB, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
                          "s_runs": [round(t, 4) for t in cpu_t]},
             "gpu_over_cpu": round(c / g, 3), "write_s": round(t_write, 2),
+            "engine": {k: st[k] for k in ("pieces_completed", "bytes_completed", "batches", "chunk_rounds",
+                                          "io_errors")},
             "sample": f"re-verify {n} x 2 MiB pieces ({total} B, linux-mint geometry, synthetic data) from one "
                       f"page-cache-warm file: vx_verify_files e2e vs the CPU pool restatement, median of {reps}"}
 

@@ -119,6 +119,7 @@ int main(int argc, char** argv) {
     polled = 0;
     bad = 0;
     sent = 0;
+    vx_reset_stats(ctx);  // the engine's own view of the timed region (vx_get_stats)
     const double t0 = now_s();
     while (sent < total) {
         std::shuffle(order.begin(), order.end(), rng);
@@ -135,13 +136,32 @@ int main(int argc, char** argv) {
     }
     if (vx_drain(ctx, 0) || poll()) return 1;
     const double el = now_s() - t0;
+    vx_stats st{};
+    vx_get_stats(ctx, &st);
+    // median batch latency from the log2 histogram: the bucket holding the middle batch
+    uint64_t acc = 0;
+    int med = 0;
+    for (int k = 0; k < VX_STATS_HIST; ++k) {
+        acc += st.batch_latency_hist[k];
+        if (2 * acc >= st.batch_latency_count) {
+            med = k;
+            break;
+        }
+    }
     if (registered)
         for (uint8_t* m : maps) vx_unregister_host_buffer(ctx, m);
     vx_destroy(ctx);
     for (uint8_t* m : maps) munmap(m, map_bytes);
     std::printf("{\"piece_len\": %u, \"pieces\": %llu, \"registered\": %d, \"flush_every\": %u, \"GiBps\": %.3f, "
-                "\"mismatched\": %llu, \"polled\": %llu}\n",
+                "\"mismatched\": %llu, \"polled\": %llu, \"engine\": {\"batches\": %llu, \"pieces_completed\": %llu, "
+                "\"gather_tiles\": %llu, \"staged_bytes\": %llu, \"submit_stall_ms\": %.3f, "
+                "\"batch_latency_mean_ms\": %.3f, \"batch_latency_max_ms\": %.3f, "
+                "\"batch_latency_median_bucket_ms\": [%.3f, %.3f]}}\n",
                 plen, (unsigned long long)total, registered, flush_every,
-                (double)total * plen / el / (1 << 30), (unsigned long long)bad, (unsigned long long)polled);
+                (double)total * plen / el / (1 << 30), (unsigned long long)bad, (unsigned long long)polled,
+                (unsigned long long)st.batches, (unsigned long long)st.pieces_completed,
+                (unsigned long long)st.gather_tiles, (unsigned long long)st.staged_bytes, st.submit_stall_ns * 1e-6,
+                st.batch_latency_count ? st.batch_latency_sum_us * 1e-3 / st.batch_latency_count : 0.0,
+                st.batch_latency_max_us * 1e-3, (double)(med ? 1ull << med : 0) * 1e-3, (double)(2ull << med) * 1e-3);
     return bad == 0 && polled == total ? 0 : 3;
 }
