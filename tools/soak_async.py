@@ -4,7 +4,10 @@ time: random piece lengths (empty to 3 MiB), pieces in registered pool
 buffers (gather kernel) and in plain memory (staged), random mismatches,
 random flush and poll cadence, pools of different piece lengths re-created
 now and then.  Every completion is checked against hashlib; any mismatch,
-loss or duplicate exits non-zero.  Prints one JSON line.
+loss or duplicate exits non-zero.  At the end of each pool the engine's
+counters (vx_get_stats) must agree with the soak's own: pieces, planted
+mismatches, bytes, staged bytes and batch-latency bookkeeping.  Prints one
+JSON line.
 
 usage: python tools/soak_async.py [--seconds 90] [--seed 1]
 """
@@ -42,6 +45,7 @@ def main():
                 pool.register_buffer(b)
             inflight = {}
             tag = 0
+            own = {"pieces": 0, "bad": 0, "bytes": 0, "staged": 0}
             for _ in range(rng.randint(50, 400)):
                 L = rng.choice([0, 1, 55, 56, 64, plen, plen, plen, rng.randint(1, plen)])
                 body = oracle.gen_piece(a.seed, tag, L)
@@ -57,6 +61,10 @@ def main():
                 exp = good if rng.random() > 0.05 else bytes(20)
                 stats["mismatches_expected"] += exp != good
                 pool.spawn(tag, 7, memoryview(buf)[:plen] if isinstance(buf, mmap.mmap) else buf, L, exp)
+                own["pieces"] += 1
+                own["bad"] += exp != good
+                own["bytes"] += L
+                own["staged"] += 0 if isinstance(buf, mmap.mmap) else L
                 inflight[tag] = (good, exp == good, buf)
                 tag += 1
                 stats["pieces"] += 1
@@ -77,6 +85,13 @@ def main():
                     return 1
             if inflight:
                 print(json.dumps({"error": "lost completions", "n": len(inflight), "plen": plen}))
+                return 1
+            st = pool.stats()
+            got = {"pieces": st["pieces_completed"], "bad": st["pieces_mismatched"], "bytes": st["bytes_completed"],
+                   "staged": st["staged_bytes"]}
+            if got != own or sum(st["batch_latency_hist"]) != st["batch_latency_count"] or \
+                    st["batch_latency_count"] != st["batches"]:
+                print(json.dumps({"error": "stats disagree", "engine": st, "soak": own, "plen": plen}))
                 return 1
             for b in bufs:
                 pool.unregister_buffer(b)
