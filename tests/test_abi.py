@@ -108,6 +108,10 @@ def test_validation_without_gpu(built):
     ctxs = (ctypes.c_void_p * 2)(None, None)
     assert L.vx_verify_files_multi(ctxs, 2, None, None, 0, 256, None, 0, None, 0) == _lib.VX_EINVAL
     assert L.vx_verify_files_multi(ctxs, 0, None, None, 0, 256, None, 0, None, 0) == _lib.VX_EINVAL
+    # observability entry points refuse NULL before touching anything
+    st = _lib.vx_stats()
+    assert L.vx_get_stats(None, ctypes.byref(st)) == _lib.VX_EINVAL
+    assert L.vx_reset_stats(None) == _lib.VX_EINVAL
 
 
 def test_sort_order_host_helper(built):
