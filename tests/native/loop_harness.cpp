@@ -204,6 +204,8 @@ int main(int argc, char** argv) {
         }
     }
     const double el = now_ms() - t0;
+    vx_stats st{};  // what the event loop would export under vortex's `metrics` feature
+    vx_get_stats(ctx, &st);
     for (uint8_t* b : pool) vx_unregister_host_buffer(ctx, b);
     vx_destroy(ctx);
     for (uint8_t* b : pool) munmap(b, plen);
@@ -212,8 +214,12 @@ int main(int argc, char** argv) {
     std::printf(
         "{\"pieces\": %u, \"piece_len\": %u, \"hashed\": %llu, \"rejected\": %llu, \"wrong\": %llu, \"turns\": %llu, "
         "\"elapsed_ms\": %.1f, \"GiBps\": %.3f, \"latency_ms_p50\": %.2f, \"latency_ms_p99\": %.2f, "
-        "\"latency_ms_max\": %.2f}\n",
+        "\"latency_ms_max\": %.2f, \"engine\": {\"pieces_completed\": %llu, \"pieces_mismatched\": %llu, "
+        "\"bytes_completed\": %llu, \"batches\": %llu, \"submit_stall_ms\": %.3f, \"batch_latency_max_ms\": %.3f}}\n",
         n, plen, (unsigned long long)hashed, (unsigned long long)rejected, (unsigned long long)wrong,
-        (unsigned long long)turns, el, bytes / (el * 1e-3) / (1 << 30), pct(0.5), pct(0.99), lat.empty() ? 0 : lat.back());
+        (unsigned long long)turns, el, bytes / (el * 1e-3) / (1 << 30), pct(0.5), pct(0.99), lat.empty() ? 0 : lat.back(),
+        (unsigned long long)st.pieces_completed, (unsigned long long)st.pieces_mismatched,
+        (unsigned long long)st.bytes_completed, (unsigned long long)st.batches, st.submit_stall_ns * 1e-6,
+        st.batch_latency_max_us * 1e-3);
     return wrong == 0 && done_count == n ? 0 : 3;
 }

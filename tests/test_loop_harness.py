@@ -31,3 +31,9 @@ def test_download_loop(built, gpu, tmp_path, n, plen, last):
     assert res["wrong"] == 0
     assert res["rejected"] == corrupted
     assert res["hashed"] == n + corrupted
+    # the engine's own counters (vx_get_stats) agree with the loop's bookkeeping
+    eng = res["engine"]
+    assert eng["pieces_completed"] == res["hashed"] and eng["pieces_mismatched"] == res["rejected"]
+    assert eng["bytes_completed"] == n * plen - (plen - last) + sum(
+        plen if i != n - 1 else last for i in range(n) if i % 50 == 25)
+    assert eng["batches"] >= 1
