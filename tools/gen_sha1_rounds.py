@@ -135,8 +135,14 @@ def _block(R: Regs, mode: str, next_slot: int, next_base: int):
     ins, final = rounds(R)
     body = emit(ins, final, R.h, feed_forward=False).splitlines()
     out = []
+    # probe-only placements (pair_probe): reads at rounds given by `at`
+    at = {"none": {}, "split2": {0: range(0, 10), 40: range(10, 20)},
+          "split4": {0: range(0, 5), 20: range(5, 10), 40: range(10, 15), 60: range(15, 20)},
+          "spread4": {4 * q: [q] for q in range(20)}, "late": {60: range(20)}}.get(mode)
     if mode == "burst":
         out += [_read(next_base, q, next_slot) for q in range(20)]
+    elif at is not None:
+        pass
     elif mode == "burst2":
         out += [f"v_add_u32_e64 {ADDR}, s25, %5"] + [_read(next_base, q, 0, ADDR) for q in range(20)]
     else:
@@ -148,13 +154,15 @@ def _block(R: Regs, mode: str, next_slot: int, next_base: int):
         if mode == "refill" and t == 16:
             out += ["s_waitcnt lgkmcnt(4)", "s_nop 0"]
         out.append(chunk[0])
+        if at is not None and t in at:
+            out += [_read(next_base, q, next_slot) for q in at[t]]
         if mode == "refill" and t < 79 and (t - 2) % 4 == 0:  # X_{4q+3} done: quad q is free
             out.append(_read(next_base, (t - 2) // 4, next_slot))
         if mode == "spread" and t < 20:  # one read per round over the first 20 rounds
             out.append(_read(next_base, t, next_slot))
         out += chunk[1:]
     out += [f"v_add_u32_e64 {h}, {h}, {f}" for h, f in zip(R.h, final)]
-    if mode in ("burst", "burst2", "spread"):
+    if mode in ("burst", "burst2", "spread") or at is not None:
         out += ["s_waitcnt lgkmcnt(0)", "s_nop 0"]
     return out
 
@@ -418,6 +426,8 @@ def main():
     ap.add_argument("--consumer6", help="write the 6-slot, barrier-per-pair consumer header (probe only: "
                                            "no faster in the kernels, DESIGN.md §3.2.1)")
     ap.add_argument("--consumerf", help="write the flag-handshake consumer header (consumer_flags_asm)")
+    ap.add_argument("--consumer-placements", help="probe only: no-barrier consumers with the ring reads placed "
+                                                  "none / split2 / split4 / spread4 / late")
     ap.add_argument("--consumer-nobarrier", help="probe only: the 3-slot consumer with every s_barrier replaced "
                                                  "by s_nop 0 (what the barrier costs; no synchronisation)")
     ap.add_argument("--mode", default="burst", choices=["refill", "burst", "burst2", "spread"],
@@ -435,6 +445,15 @@ def main():
         write_consumer_header(a.consumer6, a.mode, slots=6)
     if a.consumerf:
         write_consumerf_header(a.consumerf)
+    if a.consumer_placements:
+        with open(a.consumer_placements, "w") as f:
+            f.write("// GENERATED by tools/gen_sha1_rounds.py --consumer-placements; do not edit.\n"
+                    "// Probe only: the consumer (no barriers) with the ring reads placed per mode.\n#pragma once\n\n")
+            for m in ("none", "split2", "split4", "spread4", "late"):
+                f.write(f"#define VX_CONSUMERNB_{m.upper()}_ASM \\\n")
+                for line in consumer_asm(False, m).replace("s_barrier", "s_nop 0").splitlines():
+                    f.write(f'    "{line}\\n" \\\n')
+                f.write('    ""\n')
     if a.consumer_nobarrier:
         with open(a.consumer_nobarrier, "w") as f:
             f.write("// GENERATED by tools/gen_sha1_rounds.py --consumer-nobarrier; do not edit.\n"

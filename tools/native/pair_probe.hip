@@ -27,6 +27,9 @@
 //   16 no synchronisation: the consumer with s_barrier -> s_nop 0 and an idle
 //      producer wave (what the barriers cost; the consumer reads stale slots)
 //   17 as 16 with the producer wave running the real producer's VALU unsynchronised
+//   18-22 as 16 with the next block's 20 ring reads placed differently: none (the
+//      loop's rounds-only floor), 2 bursts of 10 (rounds 0, 40), 4 of 5 (rounds 0,
+//      20, 40, 60), one read every 4 rounds, all 20 at round 60
 // The consumer stamps s_memtime around its whole loop; prints cycles per
 // block (median over pairs) and the wall ns per block.  No HBM traffic.
 #include <hip/hip_runtime.h>
@@ -39,6 +42,7 @@
 #include "sha1_consumer6_asm.inc"  // python tools/gen_sha1_rounds.py --consumer6 tools/native/sha1_consumer6_asm.inc
 #include "sha1_consumerf_asm.inc"  // python tools/gen_sha1_rounds.py --consumerf tools/native/sha1_consumerf_asm.inc
 #include "sha1_consumernb_asm.inc"  // python tools/gen_sha1_rounds.py --consumer-nobarrier tools/native/sha1_consumernb_asm.inc
+#include "sha1_consumer_place_asm.inc"  // python tools/gen_sha1_rounds.py --consumer-placements tools/native/sha1_consumer_place_asm.inc
 
 template <int S>
 struct Ring {
@@ -179,7 +183,16 @@ __global__ __launch_bounds__(128) void pair(uint32_t nb, uint32_t* out, unsigned
     const uint32_t zero = 0;
     const uint32_t faddr = (uint32_t)(uintptr_t)&flags[0];
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
-    if (P >= 16)
+#define VX_NB(M)                                                                    \
+    asm volatile(M : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3), "+v"(h4)             \
+                 : "v"(addr), "s"(nb), "s"(nb), "v"(zero)                          \
+                 : VX_CONSUMER_ASM_CLOBBERS, "memory")
+    if (P == 18) VX_NB(VX_CONSUMERNB_NONE_ASM);
+    else if (P == 19) VX_NB(VX_CONSUMERNB_SPLIT2_ASM);
+    else if (P == 20) VX_NB(VX_CONSUMERNB_SPLIT4_ASM);
+    else if (P == 21) VX_NB(VX_CONSUMERNB_SPREAD4_ASM);
+    else if (P == 22) VX_NB(VX_CONSUMERNB_LATE_ASM);
+    else if (P >= 16)
         asm volatile(VX_CONSUMERNB_ASM
                      : "+v"(h0), "+v"(h1), "+v"(h2), "+v"(h3), "+v"(h4)
                      : "v"(addr), "s"(nb), "s"(nb), "v"(zero)
@@ -251,6 +264,11 @@ int main() {
     run<14>("real_producer_vop2_xor_2_pairs_per_cu", 512, d, dc, true);
     run<16>("no_barriers_idle_producer", 64, d, dc, true);
     run<17>("no_barriers_real_producer_unsynced", 64, d, dc, true);
+    run<18>("no_barriers_reads_none", 64, d, dc, true);
+    run<19>("no_barriers_reads_split2", 64, d, dc, true);
+    run<20>("no_barriers_reads_split4", 64, d, dc, true);
+    run<21>("no_barriers_reads_spread4", 64, d, dc, true);
+    run<22>("no_barriers_reads_late", 64, d, dc, true);
     std::printf("}\n");
     return hipDeviceSynchronize() == hipSuccess ? 0 : 1;
 }
