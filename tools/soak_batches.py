@@ -12,7 +12,6 @@ on any difference.
 usage: python tools/soak_batches.py [--seconds 120] [--seed 1]
 """
 import argparse
-import ctypes
 import json
 import mmap
 import os

@@ -30,7 +30,7 @@ from __future__ import annotations
 import ctypes
 import os
 from dataclasses import dataclass
-from typing import Any, Iterable, Optional, Sequence
+from typing import Any, Optional, Sequence
 
 from . import _lib
 from ._lib import check, lib, vx_completion, vx_config, vx_stats
