@@ -128,8 +128,17 @@ def test_verify_files_multi_contexts(built, gpu, tmp_path, nctx, pl):
         one, bad_one = pools[0].verify_files(paths, sizes, pl, exp)
         assert one == want
         for io in (0, 1, 7):
+            for p in pools:
+                p.reset_stats()
             got, bad = verify_files_multi(pools, paths, sizes, pl, exp, io_threads=io)
             assert got == want and bad == bad_one, io
+            # each context counted its own contiguous share (vx_get_stats)
+            sts = [p.stats() for p in pools]
+            assert sum(st["pieces_completed"] for st in sts) == n
+            assert sum(st["io_errors"] for st in sts) == bad
+            assert sum(st["bytes_completed"] for st in sts) == sum(sizes)
+            assert [st["pieces_completed"] for st in sts] == [n // nctx + (k >= nctx - n % nctx)
+                                                               for k in range(nctx)]
         # fewer pieces than contexts: the first contexts get empty ranges
         tiny = tmp_path / "tiny.bin"
         tiny.write_bytes(oracle.gen_piece(5, 5, pl + 1))
