@@ -430,7 +430,7 @@ def main():
                                                   "none / split2 / split4 / spread4 / late")
     ap.add_argument("--consumer-nobarrier", help="probe only: the 3-slot consumer with every s_barrier replaced "
                                                  "by s_nop 0 (what the barrier costs; no synchronisation)")
-    ap.add_argument("--mode", default="burst", choices=["refill", "burst", "burst2", "spread"],
+    ap.add_argument("--mode", default="burst", choices=["refill", "burst", "burst2", "spread", "split2", "split4", "late"],
                     help="ring-read placement (burst: the kernel's; A/B in DESIGN.md §3.2)")
     a = ap.parse_args()
     if a.check:
