@@ -495,7 +495,8 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=10,
+                    help="untimed steps first: the clock climbs for ~50 ms after the generation kernels")
     ap.add_argument("--pieces", type=int, default=65536, help="pieces per GPU")
     ap.add_argument("--piece-len", type=int, default=262144)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-thread seconds for the baseline")
