@@ -33,7 +33,14 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) {
 // hot loops; as VOP2 it flipped the 8-byte alignment of every instruction
 // after it, so ~1 in 4 of them straddled a 32-byte fetch boundary, and on
 // gfx950 each straddle cost about one issue slot.
+// -DVX_XOR2_VOP2 (A/B only): the plain 4-byte VOP2 xor.  Even with 2 or 4 waves per
+// SIMD, where a VOP2 op takes its SIMD half the cycles of a VOP3 one, it was no
+// faster (tools/ab_xor_vop2.sh, profiles/r02/negative/ab_xor_vop2.txt).
+#ifdef VX_XOR2_VOP2
+#define VX_XOR2(a, b) ((a) ^ (b))
+#else
 #define VX_XOR2(a, b) __builtin_amdgcn_bitop3_b32((a), (b), (b), 0x3C)
+#endif
 
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 
