@@ -154,6 +154,7 @@ struct vx_ctx {
     // Env overrides: VX_VERIFY_CHUNK, VX_VERIFY_RAMP, VX_VERIFY_CHUNKED_ABOVE.
     uint64_t verify_chunk = 0;
     int verify_ramp = 1;  // ramp depth d: first/last rounds C / 2^(d+1) (0 = off)
+    int verify_ramp_growth = 0;  // head ramp: 0 = rounds double, 1 = grow x5/4 (VX_VERIFY_RAMP_GROWTH)
     uint64_t verify_chunked_above = 0;
     bool verify_overlap = true;  // read round k+1 while round k is enqueued (VX_VERIFY_OVERLAP)
     uint32_t verify_readahead = 2;  // re-verify: rounds / slots read ahead of the enqueue (VX_VERIFY_READAHEAD)
@@ -762,6 +763,7 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (const char* m = std::getenv("VX_VERIFY_CHUNK"))
         c->verify_chunk = std::max<uint64_t>(4096, align_up(std::strtoull(m, nullptr, 0), 4096));
     if (const char* m = std::getenv("VX_VERIFY_RAMP")) c->verify_ramp = std::max(0, std::min(5, std::atoi(m)));
+    if (const char* m = std::getenv("VX_VERIFY_RAMP_GROWTH")) c->verify_ramp_growth = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_VERIFY_CHUNKED_ABOVE")) c->verify_chunked_above = std::strtoull(m, nullptr, 0);
     if (const char* m = std::getenv("VX_VERIFY_OVERLAP")) c->verify_overlap = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_VERIFY_COALESCE")) c->verify_coalesce = std::atoi(m) != 0;
@@ -1264,7 +1266,8 @@ struct ChunkPipe {
 // of the pipeline nothing overlaps — shrink to q.  d = 1 is C/4, C/4, C/2.
 // Every boundary is a multiple of q (>= 64 bytes for C >= 4 KiB, d <= 5), so
 // no non-final chunk ends mid-block.
-std::vector<std::pair<uint64_t, uint64_t>> chunk_schedule(uint64_t L, uint64_t C, int head, int tail) {
+std::vector<std::pair<uint64_t, uint64_t>> chunk_schedule(uint64_t L, uint64_t C, int head, int tail,
+                                                          bool gentle = false) {
     std::vector<std::pair<uint64_t, uint64_t>> r;
     const int d = std::max(head, tail);
     const uint64_t q = C >> (d + 1);
@@ -1274,7 +1277,17 @@ std::vector<std::pair<uint64_t, uint64_t>> chunk_schedule(uint64_t L, uint64_t C
     if (ramp && head) {
         r.push_back({a, q});
         a += q;
-        for (uint64_t len = q; len < C; len *= 2) r.push_back({a, len}), a += len;
+        if (gentle) {
+            // x5/4 per round, rounded up to u (4 KiB, or q when smaller): a round's
+            // read then fits under the previous round's copy, since the host reads
+            // ~1.3x faster than PCIe copies; doubling left the copy engine idle
+            // behind each larger read (profiles/r02/reverify_trace/)
+            const uint64_t u = std::min<uint64_t>(q, 4096);
+            for (uint64_t len = q; len < C; len = std::min(C, (len * 5 / 4 + u - 1) / u * u))
+                r.push_back({a, len}), a += len;
+        } else {
+            for (uint64_t len = q; len < C; len *= 2) r.push_back({a, len}), a += len;
+        }
     }
     // the tail ramp covers the last R bytes, R in (C - q, C]: C/2, ..., q, R - (C - q)
     const uint64_t tail_from = ramp && tail ? (L - C + q - 1) / q * q : L;
@@ -1322,7 +1335,8 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     for (uint64_t w0 = first; w0 < end; w0 += W) {
         const uint64_t w1 = std::min<uint64_t>(end, w0 + W);
         const uint64_t wmax = w1 == n ? std::max<uint64_t>(pl, last_len) : pl;
-        const auto sched = chunk_schedule(wmax, C, w0 == first ? c->verify_ramp : 0, w1 == end ? c->verify_ramp : 0);
+        const auto sched = chunk_schedule(wmax, C, w0 == first ? c->verify_ramp : 0, w1 == end ? c->verify_ramp : 0,
+                                          c->verify_ramp_growth != 0);
         for (size_t k = 0; k < sched.size(); ++k)
             rounds.push_back(Round{w0, w1, sched[k].first, sched[k].second, k > 0, -1, 0, 0, 0});
     }
