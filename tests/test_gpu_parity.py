@@ -498,20 +498,23 @@ def test_verify_files_chunked(built, gpu, tmp_path, pl, slot_mib, batch):
     assert not all(got) and any(got)
 
 
-@pytest.mark.parametrize("chunk,ramp,pl", [(65536, 1, 2 << 20), (262144, 1, (1 << 20) + 3072),
-                                           (131072, 0, (1 << 20) + 3072), (4096, 1, 300000),
-                                           (None, 1, 300000), (None, 1, 2 << 20), (None, 1, 262144),
-                                           (65536, 3, (1 << 20) + 3072)])
-def test_verify_files_chunk_schedule(built, gpu, tmp_path, monkeypatch, chunk, ramp, pl):
+@pytest.mark.parametrize("chunk,ramp,pl,growth", [(65536, 1, 2 << 20, 0), (262144, 1, (1 << 20) + 3072, 0),
+                                                  (131072, 0, (1 << 20) + 3072, 0), (4096, 1, 300000, 0),
+                                                  (None, 1, 300000, 0), (None, 1, 2 << 20, 0), (None, 1, 262144, 0),
+                                                  (65536, 3, (1 << 20) + 3072, 0), (None, 1, 2 << 20, 1),
+                                                  (65536, 2, (1 << 20) + 3072, 1), (4096, 1, 300000, 1)])
+def test_verify_files_chunk_schedule(built, gpu, tmp_path, monkeypatch, chunk, ramp, pl, growth):
     """Re-verify round schedules: other chunk sizes, and the
     head/tail ramp (C/4, C/4, C/2 ... C/2, C/4, rest) with piece lengths that
-    are not multiples of C/4.  Small slots force several windows, so the ramp
-    applies only to the first and last; a range call starts mid-torrent."""
+    are not multiples of C/4, and the x5/4 head ramp (VX_VERIFY_RAMP_GROWTH=1,
+    A/B option).  Small slots force several windows, so the ramp applies only
+    to the first and last; a range call starts mid-torrent."""
     from vortex_amd.hash_pool import HashPool
 
     if chunk is not None:  # None: the per-call policy (verify_chunk_for)
         monkeypatch.setenv("VX_VERIFY_CHUNK", str(chunk))
     monkeypatch.setenv("VX_VERIFY_RAMP", str(ramp))
+    monkeypatch.setenv("VX_VERIFY_RAMP_GROWTH", str(growth))
     sizes = [3 * pl + 777, 0, 5 * pl + 64, pl // 3]
     paths = []
     for k, L in enumerate(sizes):
