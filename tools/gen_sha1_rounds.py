@@ -305,7 +305,10 @@ def consumer_clobbers(select: bool, mode: str = "burst", flags: bool = False):
     v = [f"v{i}" for i in range(H0, SAVE0 + 5 if select else SAVE0)] + ([ADDR] if mode == "burst2" else [])
     v += [FLAG_V, CONS_V] if flags else []
     v += [f"v{i}" for i in range(WA, (WA if mode == "refill" else WB) + 80)]
-    return v + ["s20", "s21", "s22", "s23", "s24", "s25", "vcc"] + (["s26", "s27", "s28", "s29"] if flags else [])
+    # s_cmp_* / s_add_u32 in the loop control write SCC: name it, so the compiler
+    # never keeps a compare live in SCC across the asm body
+    return v + ["s20", "s21", "s22", "s23", "s24", "s25", "vcc", "scc"] + (["s26", "s27", "s28", "s29"] if flags
+                                                                           else [])
 
 
 def write_consumerf_header(path: str) -> None:
