@@ -118,7 +118,29 @@ int vx_unregister_host_buffer(vx_ctx* ctx, void* ptr);
  * `data` until the completion carrying `tag` has been returned by vx_poll;
  * it never frees or keeps it afterwards.  Never blocks on the GPU unless every
  * slot is in flight, in which case it waits for the oldest batch (the
- * reference's spawn never refuses work either). */
+ * reference's spawn never refuses work either).
+ *
+ * Ownership rule (vx_submit and vx_submit_piece): the piece is taken iff the
+ * call returns 0.  0 means exactly one completion carrying `tag` will come
+ * from vx_poll, or, if the context fails later, the tag is one of the
+ * vx_pending() pieces never returned (INTEGRATION.md "Device failure").  Any
+ * negative return means the piece was NOT taken: no completion will ever
+ * carry `tag`, and the caller hashes the piece elsewhere (vortex: the original
+ * scope.spawn closure).  Per code:
+ *   VX_EINVAL   NULL context or data, or (vx_submit_piece) an index outside
+ *               the piece table; the context is unchanged.
+ *   VX_ERANGE   len > max_piece_len; the context is unchanged.
+ *   VX_ENOMEM   the pinned stage for an unregistered piece could not be
+ *               allocated; the context stays usable (a later submit may
+ *               succeed, e.g. from a registered buffer).
+ *   VX_EDEVICE  a launch failed (this call's batch-full launch, or the launch
+ *               of the previous batch) or a batch failed while this call
+ *               waited for a slot.  The context is dead from now on (every
+ *               call returns the code); pieces taken earlier are recovered
+ *               through vx_poll as documented there.  If this call's own
+ *               batch launch failed part way, the device may still read
+ *               `data` until vx_destroy returns.
+ * (VX_EBUSY and VX_ENODEV are not returned by submits.) */
 int vx_submit(vx_ctx* ctx, uint64_t tag, const uint8_t* data, uint32_t len, const uint8_t* expected);
 /* Device-resident expected-digest table: upload the
  * torrent's `pieces` string (metadata.pieces, n_pieces x 20 B, the table the
@@ -126,7 +148,8 @@ int vx_submit(vx_ctx* ctx, uint64_t tag, const uint8_t* data, uint32_t len, cons
  * names a row instead of passing 20 bytes per piece.  Replaces any previous
  * table; requires no pieces in flight. */
 int vx_set_piece_table(vx_ctx* ctx, const uint8_t* table, uint32_t n_pieces);
-/* vx_submit with expected = row piece_index of the piece table. */
+/* vx_submit with expected = row piece_index of the piece table (same
+ * ownership rule and return codes). */
 int vx_submit_piece(vx_ctx* ctx, uint64_t tag, const uint8_t* data, uint32_t len, uint32_t piece_index);
 /* Launch whatever is queued (call once per event-loop turn, next to the
  * drain at event_loop.rs:554-557).  If launching would leave no batch slot
@@ -141,7 +164,8 @@ int vx_flush(vx_ctx* ctx);
  * failure the context is dead (every call returns the error), but vx_poll
  * still hands out the results of batches that did finish, and returns the
  * error only once none is left: the tags never returned are the pieces to
- * hash elsewhere (INTEGRATION.md "Device failure"). */
+ * hash elsewhere (INTEGRATION.md "Device failure"), and vx_pending() is then
+ * exactly their number. */
 int64_t vx_poll(vx_ctx* ctx, vx_completion* out, size_t max);
 /* Flush and block until every submitted piece has completed (results stay
  * queued for vx_poll).  timeout_ms = 0 waits forever. */

@@ -108,6 +108,61 @@ def interval_segments(file_lens, pl):
     return out
 
 
+def interval_segments_sweep(file_lens, pl):
+    """interval_segments in one O(files + pieces) sweep (same output): the
+    files a piece touches are a contiguous run, so each piece starts from the
+    first file that can still overlap it.  For layouts with 10^5 files."""
+    starts, acc = [], 0
+    for L in file_lens:
+        starts.append(acc)
+        acc += L
+    total = acc
+    out, f0 = [], 0
+    for p in range((total + pl - 1) // pl):
+        lo, hi = p * pl, min((p + 1) * pl, total)
+        while f0 < len(file_lens) and starts[f0] + file_lens[f0] <= lo:
+            f0 += 1
+        segs, f = [], f0
+        while f < len(file_lens) and starts[f] < hi:
+            a, b = max(lo, starts[f]), min(hi, starts[f] + file_lens[f])
+            if a < b:
+                segs.append([f, a - starts[f], b - a])
+            f += 1
+        out.append(segs)
+    return out
+
+
+def segments_text(segs) -> str:
+    """Canonical text of a segment table: one line per piece, "file offset
+    length" triples joined by ';' (tests/native/segments_dump.cpp prints it)."""
+    return "\n".join(";".join(f"{f} {o} {n}" for f, o, n in piece) for piece in segs) + "\n"
+
+
+def many_files_lens(nfiles: int = 100_000, seed: int = 100_000):
+    """A torrent of 10^5 files (not a reference layout: the scale at which a
+    per-piece walk over every file, file_store.rs:238-241, turns quadratic).
+    Mostly small files, 1 in 20 empty, 1 in 1,000 of 1-8 MiB."""
+    import random
+
+    r = random.Random(seed)
+    out = []
+    for _ in range(nfiles):
+        k = r.random()
+        out.append(0 if k < 0.05 else r.randrange(1 << 20, 8 << 20) if k > 0.999 else r.randrange(1, 40_000))
+    return out
+
+
+def many_files_layout():
+    lens = many_files_lens()
+    pl = 16384
+    segs = interval_segments_sweep(lens, pl)
+    return {"name": "many_files_100k", "source": "extra (not a reference test): tests/golden/make_golden.py "
+                                                 "many_files_lens(100000, seed 100000)",
+            "piece_length": pl, "nfiles": len(lens), "total": sum(lens), "num_pieces": len(segs),
+            "files_sha1": hashlib.sha1(" ".join(map(str, lens)).encode()).hexdigest(),
+            "segments_text_sha1": hashlib.sha1(segments_text(segs).encode()).hexdigest()}
+
+
 def file_store_layouts():
     """The reference's own FileStore layout tests and integration-test
     geometries (file path order; see the fixture's `order_note`)."""
@@ -245,6 +300,7 @@ def main(ref_root: str) -> None:
         "so the mapping is pinned whatever the order. `pieces` = hashlib over the concatenated files; "
         "`segments` = a geometric interval intersection (independent of the FileStore walk).")
     out["file_store_layouts"] = file_store_layouts()
+    out["many_files_layout"] = many_files_layout()
 
     torrent_path = os.path.join(ref_root, "cli", "linux-mint.torrent")
     if os.path.exists(torrent_path):

@@ -12,10 +12,14 @@
 * A device failure in mid-stream (injected launch failure) leaves a dead
   context that still returns every finished result, names exactly the pieces
   to re-hash, and is destroyed cleanly.
+* One ownership rule for submits (vx_hash.h): a piece is taken iff the submit
+  returns 0, so every piece comes back exactly once — polled, refused with
+  its buffer, or unfinished after a device failure.
 """
 import hashlib
 import mmap
 import random
+import time
 
 import pytest
 
@@ -180,9 +184,9 @@ def test_device_failure_recovery(built, gpu):
             pool.spawn(i, i, memoryview(pinned)[i * plen:(i + 1) * plen], plen, digests[i])
         except VxError as e:
             assert e.code == VX_EDEVICE
-            refused = i
+            refused = e.refused  # not taken: the piece comes back with the error (vx_hash.h ownership rule)
             break
-    assert refused == 23  # the third batch fills at the 24th submit and fails to launch
+    assert refused is not None and refused[0] == 23  # the third batch fills at the 24th submit and fails to launch
     time.sleep(0.5)  # the two launched batches finish
     for r in pool.try_iter():
         assert r.hash_matched and r.digest == digests[r.index]
@@ -191,9 +195,10 @@ def test_device_failure_recovery(built, gpu):
         pool.try_iter()
     assert ei.value.code == VX_EDEVICE
     assert sorted(results) == list(range(16))
+    assert pool.pending == 7  # a dead context's pending count = the pieces never returned
     lost = pool.take_unfinished()
-    assert sorted(idx for idx, _, _ in lost) == list(range(16, 23))
-    for idx, _, buf in lost + [(refused, refused, memoryview(pinned)[refused * plen:(refused + 1) * plen])]:
+    assert sorted(idx for idx, _, _ in lost) == list(range(16, 23))  # the refused piece is not among them
+    for idx, _, buf in lost + [refused]:
         assert hashlib.sha1(bytes(buf[:plen])).digest() == digests[idx]  # the caller's pool takes over
     pool.close()  # waits for the streams, then unregisters and frees
     with HashPool(plen, slots=2, batch_pieces=8) as fresh:
@@ -201,3 +206,101 @@ def test_device_failure_recovery(built, gpu):
             fresh.spawn(i, i, bytearray(bodies[i]), plen, digests[i])
         fresh.drain()
         assert sorted(r.index for r in fresh.try_iter() if r.hash_matched) == list(range(10))
+
+
+@pytest.mark.parametrize("mode", ["submit_enomem", "launch_in_submit", "launch_in_flush", "launch_two_slots"])
+def test_submit_ownership_every_tag_once(built, gpu, mode):
+    """vx_hash.h's ownership rule on the async path: a submit takes its piece
+    iff it returns 0.  Whatever fails — a non-sticky VX_ENOMEM at a submit
+    (vx_tuning_fail_submit_after), a launch failing inside vx_submit (the
+    batch-full launch), inside vx_flush, or the lazy launch inside vx_poll
+    (vx_tuning_fail_launch_after) — every piece comes back exactly once: as a
+    completion from vx_poll, as the refused piece of a failed spawn, or from
+    take_unfinished() after the context died.  Nothing is added by hand; at the
+    end vx_pending() is 0 (usable context) or the unfinished count (dead one)."""
+    from vortex_amd._lib import VX_EDEVICE, VX_ENOMEM, VxError, lib
+    from vortex_amd.hash_pool import HashPool
+
+    plen, n = 65536 + 48, 96
+    reg = mmap.mmap(-1, n * plen)  # odd pieces come from a registered (gathered) region, even ones are staged
+    bodies = [oracle.gen_piece(0x0E5, i, plen) for i in range(n)]
+    bufs = []
+    for i, b in enumerate(bodies):
+        if i % 2:
+            reg[i * plen:(i + 1) * plen] = b
+            bufs.append(memoryview(reg)[i * plen:(i + 1) * plen])
+        else:
+            bufs.append(bytearray(b))
+    digests = [hashlib.sha1(b).digest() for b in bodies]
+    exp = [d if i % 13 else bytes(20) for i, d in enumerate(digests)]  # some planted mismatches
+    # slots=2: vx_flush defers its launch while the other slot is in flight (DESIGN.md §6.5), so the
+    # failing launch may be vx_poll's lazy one as well as vx_flush's or vx_submit's
+    pool = HashPool(plen, slots=2 if mode == "launch_two_slots" else 3, batch_pieces=8)
+    pool.register_buffer(reg)
+    if mode == "submit_enomem":
+        fails = {5, 6, 30, 71}  # non-sticky: the context stays usable after each
+    elif mode == "launch_in_submit":
+        lib().vx_tuning_fail_launch_after(pool._h, 2)
+    else:
+        lib().vx_tuning_fail_launch_after(pool._h, 3)
+    seen: dict[int, str] = {}
+    dead = False
+
+    def take(results):
+        for r in results:
+            assert r.index not in seen, f"piece {r.index} returned twice"
+            seen[r.index] = "polled"
+            assert r.digest == digests[r.index]
+            assert r.hash_matched == (exp[r.index] == digests[r.index])
+
+    for i in range(n):
+        if mode == "submit_enomem" and i in fails:
+            lib().vx_tuning_fail_submit_after(pool._h, 0)
+        try:
+            pool.spawn(i, 7, bufs[i], plen, exp[i])
+        except VxError as e:
+            assert e.refused is not None and e.refused[0] == i and e.refused[2] is bufs[i]
+            assert i not in seen
+            seen[i] = "refused"
+            if e.code == VX_EDEVICE:
+                dead = True
+                break
+            assert mode == "submit_enomem" and e.code == VX_ENOMEM and i in fails
+            continue
+        if mode != "launch_in_submit" and i % 5 == 4:  # the event loop's turn: flush, then drain
+            try:
+                pool.flush()
+                take(pool.try_iter())
+            except VxError as e:
+                assert e.code == VX_EDEVICE
+                dead = True
+                break
+    if not dead:
+        assert mode == "submit_enomem"
+        pool.drain()
+        take(pool.try_iter())
+        assert pool.pending == 0
+    else:
+        assert mode != "submit_enomem"
+        time.sleep(0.3)  # batches launched before the failure finish
+        while True:  # a dead context hands out every finished result, then the error
+            try:
+                got = pool.try_iter()
+            except VxError as e:
+                assert e.code == VX_EDEVICE
+                break
+            take(got)
+        unfinished = pool.pending
+        lost = pool.take_unfinished()
+        assert len(lost) == unfinished
+        for idx, conn, buf in lost:
+            assert idx not in seen, f"piece {idx} both returned and unfinished"
+            assert conn == 7 and buf is bufs[idx]
+            seen[idx] = "unfinished"
+    submitted = max(seen) + 1
+    assert sorted(seen) == list(range(submitted)), "every submitted piece comes back exactly once"
+    if mode == "submit_enomem":
+        assert submitted == n and sorted(i for i, how in seen.items() if how == "refused") == sorted(fails)
+    else:
+        assert list(seen.values()).count("refused") <= 1 and "unfinished" in seen.values()
+    pool.close()

@@ -33,7 +33,9 @@ INTS = {"u8", "u16", "u32", "u64", "usize", "i8", "i16", "i32", "i64", "isize", 
 
 REF_NAMES = {"metadata": "Torrent", "index": "i32", "conn_id": "ConnectionId", "buffer": "Buffer",
              "piece_len": "u32", "root": "PathBuf", "num_gpus": "usize", "initialized_state": "InitializedState",
-             "torrent_state": "InitializedState", "file_store": "FileStore"}
+             "torrent_state": "InitializedState", "file_store": "FileStore",
+             # rayon::Scope opened at event_loop.rs:385, passed down to handle_message (peer_connection.rs:631-637)
+             "scope": "Scope"}
 REF_FIELDS = {("Torrent", "pieces"): "Vec<Vec<u8>>", ("Torrent", "piece_length"): "i64",
               ("Torrent", "length"): "i64", ("Torrent", "name"): "String",
               ("Torrent", "files"): "Option<Vec<File>>",
@@ -270,6 +272,8 @@ class Checker:
                     except Untyped as e:
                         problems.append(f"{recv}.{name}: receiver untyped ({e})")
                         continue
+                    if rt == "Scope" and name == "spawn":
+                        continue  # rayon's Scope::spawn: the reference's own closure, not the binding
                     if rt != "GpuHasher":
                         problems.append(f"{recv}.{name}: receiver is {rt}, not GpuHasher")
                         continue
@@ -339,3 +343,39 @@ def test_checker_rejects_known_mistakes(bad, needle):
              "let lens: Vec<u64> = x;\nlet mut matched: Vec<u8> = x;\n" + bad)
     _, problems = Checker(blocks + [extra]).check()
     assert any(needle in p for p in problems), problems
+
+
+def test_refused_spawn_hands_the_buffer_back():
+    """vx_hash.h's ownership rule at the Rust boundary: a submit that returns
+    non-zero did not take the piece, so GpuHasher::spawn / spawn_indexed must
+    return the Buffer in the Err (and insert into `inflight` only on success),
+    and every call site must bind that Buffer and hash the piece itself — a
+    dropped Err would strand a piece vortex already marked downloaded
+    (peer_connection.rs:1140) and trip BufferPool's leak check (buf_pool.rs:21-30)."""
+    blocks = rust_blocks()
+    impl = re.search(r"impl GpuHasher \{(.*?)\n\}", blocks[0], flags=re.S).group(1)
+    for name in ("spawn", "spawn_indexed"):
+        m = re.search(rf"pub fn {name}\(.*?\)\s*->\s*([^{{]+?)\s*\{{(.*?)\n    \}}", impl, flags=re.S)
+        assert m, name
+        assert norm(m.group(1)) == "Result<(), (i64, usize, ConnectionId, Buffer)>", (name, m.group(1))
+        body = m.group(2)
+        ret = body.find("return Err((rc as i64, index, conn_id, buffer))")
+        ins = body.find("self.inflight.insert(")
+        assert 0 <= ret < ins, f"{name}: the refused piece must return before it enters inflight"
+    sites = 0
+    for block in blocks[1:]:
+        code = re.sub(r"//[^\n]*", "", block)
+        for m in re.finditer(r"\.(spawn|spawn_indexed)\s*\(", code):
+            recv = re.search(r"([\w.]+)$", code[:m.start()]).group(1)
+            if not recv.endswith("hasher"):
+                continue
+            sites += 1
+            head = code[:m.start()]
+            b = re.search(r"if let Err\(\((\w+), (\w+), (\w+), (\w+)\)\) =\s*[\w.]+$", head)
+            assert b, f"{recv}.{m.group(1)}: the Err (with the Buffer) must be bound"
+            rest = code[matching(code, m.end() - 1):]
+            body = rest[rest.index("{"):]
+            body = body[:matching(body, 0) + 1]
+            assert re.search(rf"\b{b.group(4)}\b", body), "the returned Buffer must be used (hashed and handed on)"
+            assert "complete_tx.send(" in body, "a refused piece must still produce its DownloadedPiece"
+    assert sites >= 1

@@ -47,6 +47,8 @@ class VxError(RuntimeError):
     def __init__(self, code: int, where: str, msg: str):
         super().__init__(f"{where} failed: {code} ({msg})")
         self.code = code
+        # HashPool.spawn: (index, conn_id, buffer) of a piece the engine did not take
+        self.refused = None
 
 
 class vx_completion(ctypes.Structure):

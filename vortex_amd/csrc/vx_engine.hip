@@ -202,6 +202,10 @@ struct vx_ctx {
     // device error would, turning the context sticky; < 0 = off.
     int64_t fail_launch_after = -1;
     vx_stats stats{};  // vx_get_stats (observability counters)
+    // harvest() counts mismatches unless the caller overrides verdicts after
+    // it (the file re-verify: a piece with an I/O error is counted in
+    // io_errors only, FileVerify::consume counts the final verdicts)
+    bool harvest_counts_mismatches = true;
 };
 
 namespace {
@@ -554,7 +558,7 @@ void harvest(vx_ctx* c, Slot& s) {
     }
     if (s.n) {
         c->stats.pieces_completed += s.n;
-        c->stats.pieces_mismatched += bad;
+        if (c->harvest_counts_mismatches) c->stats.pieces_mismatched += bad;
         c->stats.bytes_completed += bytes;
         record_batch_latency(c, s.t_open);
     }
@@ -693,7 +697,19 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
     s->n = i + 1;
     s->bytes = off + std::max<uint32_t>(len, 1);
     c->pending++;
-    if (s->n >= c->cfg.batch_pieces && !c->bulk) return launch_slot(c, si);
+    if (s->n >= c->cfg.batch_pieces && !c->bulk) {
+        if (int rc = launch_slot(c, si)) {
+            // One rule for every submit (vx_hash.h): a non-zero return means
+            // the piece was NOT taken.  The launch failed (the context is now
+            // sticky), so this piece leaves the batch again and goes back to
+            // the caller with the error; the rest of the slot stays pending and
+            // is what the caller recovers after vx_poll reports the failure.
+            s->tags.pop_back();
+            s->n = i;
+            c->pending--;
+            return rc;
+        }
+    }
     return 0;
 }
 
@@ -973,6 +989,7 @@ struct FileVerify {
         while (!c->done.empty()) {
             const vx_completion& r = c->done.front();
             matched_out[r.tag] = (r.matched && !bad[r.tag]) ? 1 : 0;
+            c->stats.pieces_mismatched += !r.matched && !bad[r.tag];  // I/O errors count in io_errors only
             c->done.pop_front();
             ++done;
         }
@@ -1225,8 +1242,10 @@ struct ChunkPipe {
     }
     void end_window() { have_prev = false; }  // windows hold disjoint pieces
 
-    // Wait for every round, then copy verdicts / digests back (either may be NULL).
-    int finish(uint8_t* matched_out, uint8_t* digests_out, int rc) {
+    // Wait for every round, then copy verdicts / digests back (either may be
+    // NULL).  bad (may be NULL): pieces the caller fails for an I/O error,
+    // counted in io_errors and not again as mismatches.
+    int finish(uint8_t* matched_out, uint8_t* digests_out, int rc, const uint8_t* bad = nullptr) {
         if (!rc) {
             for (auto& s : c->slots)
                 if (s.state == Slot::INFLIGHT && hipEventSynchronize(s.done) != hipSuccess) rc = VX_EDEVICE;
@@ -1240,7 +1259,7 @@ struct ChunkPipe {
             c->stats.pieces_completed += cnt;
             c->stats.bytes_completed += bytes;
             if (matched_out && d_match)
-                for (uint64_t i = 0; i < cnt; ++i) c->stats.pieces_mismatched += matched_out[i] == 0;
+                for (uint64_t i = 0; i < cnt; ++i) c->stats.pieces_mismatched += matched_out[i] == 0 && !(bad && bad[i]);
         }
         for (auto& s : c->slots)
             if (s.state == Slot::INFLIGHT) {
@@ -1426,7 +1445,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
             reset_fill(sl);
             sl.state = Slot::FREE;
         }
-    rc = cp.finish(fv.matched_out, nullptr, rc);
+    rc = cp.finish(fv.matched_out, nullptr, rc, fv.bad.data());
     if (trace && !tev.empty()) {
         float t0 = 0, a = 0, b = 0;
         size_t k = 0;
@@ -1806,6 +1825,7 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
     {
         vx_files::Readers rd(nthreads, fs, fds, piece_length, bad.data(), first);
         FileVerify fv{c, expected, matched_out, bad};
+        c->harvest_counts_mismatches = false;
         rc = chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total, first, end, C)
                      : verify_whole(fv, rd, n_pieces, piece_length, total, first, end);
         if (!rc && !chunked) {
@@ -1817,11 +1837,18 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
                 if (!any && fv.done < count && !rc) rc = fail(VX_EDEVICE, "vx_verify_files: lost completions");
             }
         }
+        c->harvest_counts_mismatches = true;
         if (rc) {
+            // The call fails and its results are dropped: wait for every slot
+            // still reading the stages, then free them without harvest(), so
+            // abandoned pieces never reach vx_stats.
             for (auto& s : c->slots)
                 if (s.state == Slot::INFLIGHT) (void)hipEventSynchronize(s.done);
             for (auto& s : c->slots)
-                if (s.state == Slot::INFLIGHT) harvest(c, s);
+                if (s.state == Slot::INFLIGHT) {
+                    reset_fill(s);
+                    s.state = Slot::FREE;
+                }
             c->done.clear();
         }
     }

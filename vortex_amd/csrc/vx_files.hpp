@@ -58,11 +58,23 @@ struct Seg {
 };
 
 // FileStore::check_piece_hash_sync's segment walk (file_store.rs:240-298).
+// The reference filters every file of the torrent for each piece
+// (files.iter().filter(start_piece <= idx <= end_piece), file_store.rs:238-241),
+// which is O(files) per piece and quadratic over a re-verify of a torrent with
+// 10^4-10^5 files.  layout() makes start_piece and end_piece non-decreasing in
+// the file index (file f+1 starts where file f ends), so the files the filter
+// keeps are one contiguous run: the first file with end_piece >= piece (binary
+// search) up to the last with start_piece <= piece.  Same files, same order,
+// same segments as the walk (tests/test_native_cpu.py checks 10^5 files).
 inline void segments(const std::vector<FileSpan>& fs, int64_t piece, uint32_t piece_length, std::vector<Seg>& out) {
     out.clear();
     int64_t total = 0;
-    for (size_t f = 0; f < fs.size(); ++f) {
+    const size_t f0 = (size_t)(std::lower_bound(fs.begin(), fs.end(), piece,
+                                                [](const FileSpan& s, int64_t p) { return s.end_piece < p; }) -
+                               fs.begin());
+    for (size_t f = f0; f < fs.size(); ++f) {
         const FileSpan& s = fs[f];
+        if (s.start_piece > piece) break;  // and so does every later file
         if (!(s.start_piece <= piece && piece <= s.end_piece)) continue;
         const int64_t file_index = piece - s.start_piece;
         const int64_t file_offset = file_index * (int64_t)piece_length - s.start_offset;

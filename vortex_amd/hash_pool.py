@@ -33,7 +33,7 @@ from dataclasses import dataclass
 from typing import Any, Optional, Sequence
 
 from . import _lib
-from ._lib import check, lib, vx_completion, vx_config, vx_stats
+from ._lib import VxError, check, lib, vx_completion, vx_config, vx_stats
 
 
 @dataclass
@@ -140,7 +140,14 @@ class HashPool:
     def spawn(self, index: int, conn_id: int, buffer, piece_len: int, expected_hash: Optional[bytes] = None) -> None:
         """peer_connection.rs:1145-1158: hash buffer[:piece_len] against
         expected_hash (or, when None, against row `index` of the table given
-        to set_piece_table); the result comes back from try_recv()."""
+        to set_piece_table); the result comes back from try_recv().
+
+        Ownership (include/vx_hash.h): the piece is taken iff the submit
+        returns 0.  Otherwise this raises VxError whose ``refused`` is
+        ``(index, conn_id, buffer)``: the piece was not taken, no result will
+        ever carry it, it is not in take_unfinished(), and the caller hashes
+        it on its own pool.  On VX_EDEVICE the pool is dead: collect the rest
+        with try_iter() until it raises, then take_unfinished()."""
         if expected_hash is not None and len(expected_hash) != 20:
             raise ValueError("expected_hash must be 20 bytes")
         addr, keep = _addr_of(buffer)
@@ -149,10 +156,16 @@ class HashPool:
         tag = self._next_tag
         self._next_tag += 1
         if expected_hash is None:
-            check(lib().vx_submit_piece(self._h, tag, addr, piece_len, index), "vx_submit_piece")
+            rc, where = lib().vx_submit_piece(self._h, tag, addr, piece_len, index), "vx_submit_piece"
         else:
             exp = ctypes.create_string_buffer(bytes(expected_hash), 20)
-            check(lib().vx_submit(self._h, tag, addr, piece_len, exp), "vx_submit")
+            rc, where = lib().vx_submit(self._h, tag, addr, piece_len, exp), "vx_submit"
+        if rc != 0:
+            try:
+                check(rc, where)
+            except VxError as e:
+                e.refused = (index, conn_id, buffer)
+                raise
         self._inflight[tag] = (index, conn_id, buffer, keep)
 
     def set_piece_table(self, pieces: bytes) -> None:
@@ -185,17 +198,24 @@ class HashPool:
         """Everything completed so far (the `while let Ok(..) = try_recv()` loop)."""
         out = []
         while True:
-            got = self._poll(len(self._cbuf))
+            try:
+                got = self._poll(len(self._cbuf))
+            except VxError:
+                if out:  # hand out what was already taken off the engine; the error is sticky
+                    return out  # and the next call raises it
+                raise
             out.extend(got)
             if len(got) < len(self._cbuf):
                 return out
 
     def take_unfinished(self) -> list[tuple[int, int, Any]]:
         """After a device error (a VxError from spawn / try_recv / try_iter):
-        (index, conn_id, buffer) of every submitted piece whose result never
-        came back, for the caller to hash on its own pool (INTEGRATION.md
-        "Device failure").  Close the pool before reusing those buffers: that
-        waits for the device to stop reading them."""
+        (index, conn_id, buffer) of every TAKEN piece whose result never came
+        back, for the caller to hash on its own pool (INTEGRATION.md "Device
+        failure").  A spawn that raised did not take its piece (it is in the
+        exception's ``refused``), so it is not listed here.  Close the pool
+        before reusing those buffers: that waits for the device to stop
+        reading them."""
         out = [(index, conn_id, buffer) for index, conn_id, buffer, _keep in self._inflight.values()]
         self._inflight.clear()
         return out
