@@ -24,11 +24,21 @@ Extra fields (DESIGN.md §7 "Measurement"; all but roofline at N=1 only):
                  mmaps (vortex's BufferPool layout) via vx_verify_batch.
   e2e_async      the same pieces through vx_submit/vx_flush/vx_poll.
   e2e_contiguous the same pieces in one registered mmap (best-case layout).
-  reverify       config 5: linux-mint-geometry re-verify from a file via
-                 vx_verify_files, with the CPU pool on the same file.
+  reverify       config 5: linux-mint-geometry re-verify from an fsync'd,
+                 page-cache-warm file via vx_verify_files, with the CPU pool
+                 on the same file, and each call's read / copy budget.
+  reverify_cold  the same with the file's pages evicted before every call
+                 (fsync + POSIX_FADV_DONTNEED): reads from the disk.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-(N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+N > 1: either launched by the driver as
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+or started plainly, in which case bench.py starts the N ranks itself (a
+child torch.distributed.run, before any GPU call) and relays rank 0's line
+and exit code.  --gpus must equal WORLD_SIZE when one is set, and a run that
+cannot get N ranks fails: it never prints a one-GPU line for --gpus N.
+Whenever it runs under torch.distributed (even WORLD_SIZE=1) the process
+group is real and the line reports its world_size and backend.
 """
 from __future__ import annotations
 
@@ -345,7 +355,72 @@ def ragged_leg(dev, stream, steps: int = 5):
                       "device-resident, verify vs expected table, median of %d launches" % steps}
 
 
-def reverify_leg(reps: int = 3):
+def fs_type(path: str) -> str:
+    """Filesystem type of the mount holding `path` (longest /proc/mounts prefix)."""
+    best, kind = "", "?"
+    try:
+        with open("/proc/mounts") as f:
+            for line in f:
+                parts = line.split()
+                if len(parts) >= 3 and (path == parts[1] or path.startswith(parts[1].rstrip("/") + "/")) \
+                        and len(parts[1]) > len(best):
+                    best, kind = parts[1], parts[2]
+    except OSError:
+        pass
+    return kind
+
+
+def resident_fraction(path: str) -> float | None:
+    """Fraction of the file's pages in the page cache (mmap + mincore; maps
+    without touching the pages)."""
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.mmap.restype = ctypes.c_void_p
+    libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_long]
+    libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    libc.mincore.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    size = os.path.getsize(path)
+    if size == 0:
+        return None
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        addr = libc.mmap(None, size, mmap.PROT_READ, mmap.MAP_SHARED, fd, 0)
+        if addr in (None, ctypes.c_void_p(-1).value):
+            return None
+        try:
+            pages = (size + mmap.PAGESIZE - 1) // mmap.PAGESIZE
+            vec = (ctypes.c_ubyte * pages)()
+            if libc.mincore(addr, size, vec) != 0:
+                return None
+            return sum(b & 1 for b in bytes(vec)) / pages
+        finally:
+            libc.munmap(addr, size)
+    finally:
+        os.close(fd)
+
+
+def drop_cache(path: str) -> float | None:
+    """Write back and evict the file's pages (fsync + POSIX_FADV_DONTNEED; no
+    privilege needed), return the resident fraction left."""
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        os.fsync(fd)
+        os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+    finally:
+        os.close(fd)
+    return resident_fraction(path)
+
+
+def reverify_dir() -> str:
+    """Where the config-5 file goes: the first candidate on a disk-backed
+    filesystem (a 'cold' read from tmpfs would still be a memory copy)."""
+    cands = [os.environ.get("TMPDIR", ""), "/var/tmp", "/tmp", os.path.join(ROOT, "gpurun_out"), ROOT]
+    for d in cands:
+        if d and os.path.isdir(d) and os.access(d, os.W_OK) and fs_type(d) not in ("tmpfs", "ramfs"):
+            return d
+    return next(d for d in cands if d and os.path.isdir(d) and os.access(d, os.W_OK))
+
+
+def reverify_leg(reps: int = 3, cold_reps: int = 2):
     """BASELINE config 5: full re-verify of a torrent's data from disk with
     the linux-mint geometry (cli/linux-mint.torrent: 2,907,832,320 B, 2 MiB
     pieces, last 1,179,648 B) through vx_verify_files (pread into pinned
@@ -353,7 +428,16 @@ def reverify_leg(reps: int = 3):
     vortex's own re-verify (par_iter over check_piece_hash_sync,
     oracle/pool_oracle.cpp) on the same file and host cores.  The ISO is
     not available offline: a synthetic file of identical geometry is written
-    first (page-cache warm for both legs)."""
+    first, then fsync'd so no writeback overlaps the timed calls.
+
+    Two legs, each GPU and CPU pool alternating per rep:
+      warm  the file's pages in the page cache (vortex re-verifying data it
+            just wrote or read);
+      cold  every call preceded by fsync + POSIX_FADV_DONTNEED, so the reads
+            go to the disk (vortex starting up on a torrent whose data is not
+            cached); the resident fraction before each call is recorded.
+    Each GPU call's time budget (vx_tuning_last_verify: reader busy time and
+    rate, GPU-timed copy busy fraction) goes into the record."""
     import oracle
     from vortex_amd.hash_pool import HashPool
 
@@ -361,45 +445,78 @@ def reverify_leg(reps: int = 3):
     n = (total + pl - 1) // pl
     last = total - (n - 1) * pl
     threads = cpu_share()
-    tmp = os.environ.get("TMPDIR", "/tmp")
-    path = os.path.join(tmp, f"vx_bench_linuxmint_{os.getpid()}.iso")
+    d = reverify_dir()
+    path = os.path.join(d, f"vx_bench_linuxmint_{os.getpid()}.iso")
     buf = ctypes.create_string_buffer(pl)
     t0 = time.perf_counter()
+
+    def trace_of(pool):
+        tr = pool.last_verify()
+        keep = ("wall_ms", "read_busy_ms", "read_span_ms", "first_read_ms", "copy_busy_ms", "copy_span_ms", "tail_ms",
+                "read_GiBps", "read_GiBps_per_thread", "copy_GiBps", "copy_busy_frac", "rounds", "readers")
+        return {k: (round(tr[k], 3) if isinstance(tr[k], float) else tr[k]) for k in keep}
+
     try:
         with open(path, "wb") as f:
             for i in range(n):
                 L = last if i == n - 1 else pl
                 oracle.lib().vxo_gen_piece(0x5EED0005, i, L, 0, buf)
                 f.write(memoryview(buf)[:L])
+            f.flush()
+            os.fsync(f.fileno())  # writeback done before anything is timed
         t_write = time.perf_counter() - t0
         exp = oracle.pool_digest_synth(0x5EED0005, 0, n, pl, last_index=n - 1, last_len=last, threads=threads)
-        gpu_t, cpu_t = [], []
+        legs = {}
         with HashPool(pl, slots=4, slot_bytes=512 << 20, batch_pieces=4096) as pool:
-            got, bad = pool.verify_files([path], [total], pl, exp, io_threads=threads)  # warm (stages, rows)
+            got, bad = pool.verify_files([path], [total], pl, exp, io_threads=threads)  # warm (stages, rows, cache)
             assert all(got) and bad == 0
             pool.reset_stats()
-            for _ in range(reps):
-                t0 = time.perf_counter()
-                got, bad = pool.verify_files([path], [total], pl, exp, io_threads=threads)
-                gpu_t.append(time.perf_counter() - t0)
-                assert all(got) and bad == 0
-                t0 = time.perf_counter()
-                cpu = oracle.pool_verify_files([path], [total], pl, exp, threads=threads)
-                cpu_t.append(time.perf_counter() - t0)
-                assert all(cpu)
+            for leg in ("warm", "cold"):
+                gpu_t, cpu_t, traces, resident = [], [], [], []
+                for _ in range(reps if leg == "warm" else cold_reps):
+                    if leg == "cold":
+                        resident.append(drop_cache(path))
+                    else:
+                        resident.append(resident_fraction(path))
+                    t0 = time.perf_counter()
+                    got, bad = pool.verify_files([path], [total], pl, exp, io_threads=threads)
+                    gpu_t.append(time.perf_counter() - t0)
+                    assert all(got) and bad == 0
+                    traces.append(trace_of(pool))
+                    if leg == "cold":
+                        resident.append(drop_cache(path))
+                    t0 = time.perf_counter()
+                    cpu = oracle.pool_verify_files([path], [total], pl, exp, threads=threads)
+                    cpu_t.append(time.perf_counter() - t0)
+                    assert all(cpu)
+                legs[leg] = (gpu_t, cpu_t, traces, resident)
             st = pool.stats()
     finally:
         if os.path.exists(path):
             os.unlink(path)
-    g, c = sorted(gpu_t)[len(gpu_t) // 2], sorted(cpu_t)[len(cpu_t) // 2]
-    return {"value": round(total / g / GiB, 2), "unit": "GiB/s", "gpu_s_runs": [round(t, 4) for t in gpu_t],
-            "cpu_pool": {"value": round(total / c / GiB, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
-                         "s_runs": [round(t, 4) for t in cpu_t]},
-            "gpu_over_cpu": round(c / g, 3), "write_s": round(t_write, 2),
-            "engine": {k: st[k] for k in ("pieces_completed", "bytes_completed", "batches", "chunk_rounds",
-                                          "io_errors")},
-            "sample": f"re-verify {n} x 2 MiB pieces ({total} B, linux-mint geometry, synthetic data) from one "
-                      f"page-cache-warm file: vx_verify_files e2e vs the CPU pool restatement, median of {reps}"}
+
+    def record(leg):
+        gpu_t, cpu_t, traces, resident = legs[leg]
+        g, c = sorted(gpu_t)[len(gpu_t) // 2], sorted(cpu_t)[len(cpu_t) // 2]
+        return {"value": round(total / g / GiB, 2), "unit": "GiB/s", "gpu_s_runs": [round(t, 4) for t in gpu_t],
+                "cpu_pool": {"value": round(total / c / GiB, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
+                             "s_runs": [round(t, 4) for t in cpu_t]},
+                "gpu_over_cpu": round(c / g, 3),
+                "resident_before_calls": [None if r is None else round(r, 4) for r in resident],
+                "gpu_traces": traces}
+
+    warm, cold = record("warm"), record("cold")
+    where = {"dir": d, "fs": fs_type(d)}
+    warm.update({"write_s": round(t_write, 2), "file": where,
+                 "engine": {k: st[k] for k in ("pieces_completed", "bytes_completed", "batches", "chunk_rounds",
+                                               "io_errors")},
+                 "sample": f"re-verify {n} x 2 MiB pieces ({total} B, linux-mint geometry, synthetic data) from one "
+                           f"fsync'd, page-cache-warm file: vx_verify_files e2e vs the CPU pool restatement, "
+                           f"alternating, median of {reps}"})
+    cold.update({"file": where,
+                 "sample": f"the same file with fsync + POSIX_FADV_DONTNEED before every call (reads from "
+                           f"{where['fs']}), GPU and CPU pool alternating, median of {cold_reps}"})
+    return warm, cold
 
 
 def roofline(n: int, plen: int, kern_ms: float, achieved: float, workload: str) -> dict:
@@ -491,6 +608,54 @@ def roofline(n: int, plen: int, kern_ms: float, achieved: float, workload: str) 
                              "128 KiB) run no faster (DESIGN.md §4)"}}
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def launch_cmd(args, argv, port: int) -> list:
+    """The child launch of a plain `bench.py --gpus N` (N > 1): one rank per
+    GPU on this node through torch.distributed.run, same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(args, argv) -> int:
+    """Start args.gpus ranks as a child process group and relay rank 0's JSON
+    line and the exit code.  Runs before anything touches the GPU (counting
+    devices does not initialise it on this ROCm build), and never execs."""
+    import subprocess
+
+    if not args.same_device:
+        import torch
+
+        ndev = torch.cuda.device_count()
+        if ndev < args.gpus:
+            log(f"error: --gpus {args.gpus} but only {ndev} GPU(s) visible; refusing to report a smaller run")
+            return 2
+    cmd = launch_cmd(args, argv, _free_port())
+    log("launching", args.gpus, "ranks:", " ".join(cmd))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    lines = []
+    for line in p.stdout:  # stream: a long run keeps printing (stderr is inherited)
+        sys.stdout.write(line)
+        sys.stdout.flush()
+        lines.append(line)
+    rc = p.wait()
+    if rc != 0:
+        log(f"error: the {args.gpus}-rank run failed (rc {rc})")
+        return rc
+    res = [json.loads(x) for x in lines if x.startswith("{")]
+    if len(res) != 1 or res[0].get("n_gpus") != args.gpus or res[0].get("world_size") != args.gpus:
+        log(f"error: expected one result line with n_gpus = world_size = {args.gpus}, got {len(res)}")
+        return 1
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -509,6 +674,18 @@ def main() -> int:
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank uses cuda:0 (with --dist-backend gloo)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+
+    # N ranks or nothing: a plain `bench.py --gpus N` launches its own ranks
+    # (before any GPU call); under a launcher, WORLD_SIZE must be N.
+    distributed = "WORLD_SIZE" in os.environ
+    if not distributed and args.gpus > 1:
+        return launch_ranks(args, sys.argv[1:])
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE {world}")
+        return 2
 
     import torch
     import torch.distributed as dist
@@ -516,20 +693,21 @@ def main() -> int:
     from vortex_amd import device as vdev
     from vortex_amd.shard import gather_verdicts
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
     if args.same_device:
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if distributed:  # a real process group, even at WORLD_SIZE=1 (exercises RCCL init and the gather)
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.dist_backend)
+        backend = dist.get_backend()
+        assert dist.get_world_size() == world
+    else:
+        backend = None
 
     n, plen = args.pieces, args.piece_len
     stride = (plen + 15) // 16 * 16
@@ -560,12 +738,12 @@ def main() -> int:
 
     for _ in range(args.warmup):
         step()
-        if world > 1:
+        if distributed:
             gather_verdicts(matched, n_total)
     torch.cuda.synchronize()
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -574,15 +752,15 @@ def main() -> int:
         evs[k][0].record(stream)
         step()
         evs[k][1].record(stream)
-        if world > 1:
+        if distributed:
             verdicts = gather_verdicts(matched, n_total)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = t1 - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
                          device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -605,6 +783,8 @@ def main() -> int:
         "value": round(value, 2),
         "unit": "GiB/s",
         "n_gpus": world,
+        "world_size": dist.get_world_size() if distributed else 1,
+        "backend": backend,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
@@ -614,7 +794,7 @@ def main() -> int:
         "dtype": "u32",
         "data": "synthetic: counter-based splitmix64 pieces generated in HBM, 1% with one flipped byte",
         "config": {"workload": workload + " (BASELINE config 2; config 4 at N=8), SHA-1 + verify vs expected table"
-                               + (", RCCL all-gather of verdicts" if world > 1 else ""),
+                               + (f", {backend} all-gather of verdicts" if distributed else ""),
                    "pieces_per_gpu": n, "piece_len": plen, "total_GiB": round(total_bytes / GiB, 2),
                    "parallelism": f"piece-index shard x{world}"},
         "roofline": roofline(n, plen, kern_ms, achieved, workload),
@@ -639,12 +819,12 @@ def main() -> int:
             res["e2e_contiguous"] = e2e_contiguous(plen)
             log("e2e contiguous:", res["e2e_contiguous"]["value"], "GiB/s")
         if not args.no_reverify:
-            res["reverify"] = reverify_leg()
-            log("reverify (config 5):", res["reverify"]["value"], "GiB/s; CPU pool",
-                res["reverify"]["cpu_pool"]["value"])
+            res["reverify"], res["reverify_cold"] = reverify_leg()
+            for k in ("reverify", "reverify_cold"):
+                log(f"{k} (config 5):", res[k]["value"], "GiB/s; CPU pool", res[k]["cpu_pool"]["value"])
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
     return 0
 

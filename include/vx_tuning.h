@@ -46,6 +46,25 @@ int vx_tuning_plan_ragged(uint32_t n, uint32_t max_len, uint64_t total_len);
  * (2*max uint64_t) and returns the number of rounds (host-only). */
 size_t vx_tuning_chunk_schedule(uint64_t L, uint64_t C, int head, int tail, uint64_t* out, size_t max);
 
+/* Where the last vx_verify_files / vx_verify_files_range call on ctx spent
+ * its time (bench.py records it per timed call).  Host times
+ * are steady-clock; copy times are the GPU's own (events around each data
+ * H2D) and exist only on the resumable chunk path (pieces >= 2 chunks). */
+typedef struct vx_verify_trace {
+    double wall_ms;        /* the whole call                                          */
+    double read_busy_ms;   /* pread time summed over the reader threads               */
+    double read_span_ms;   /* first read started -> last read finished                */
+    double first_read_ms;  /* call start -> first read finished (nothing overlaps it) */
+    double copy_busy_ms;   /* GPU-timed data copies, summed (chunk path)              */
+    double copy_span_ms;   /* first copy start -> last copy end, GPU clock            */
+    double tail_ms;        /* last round enqueued -> verdicts on the host             */
+    uint64_t read_bytes;   /* bytes pread                                             */
+    uint64_t copy_bytes;   /* bytes of the timed copies                               */
+    uint32_t readers;      /* reader threads                                          */
+    uint32_t rounds;       /* timed copies (chunk rounds)                             */
+} vx_verify_trace;
+int vx_tuning_last_verify(const struct vx_ctx* ctx, vx_verify_trace* out);
+
 int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
                                    const void* d_expected, void* d_matched, void* stream, int variant);
 

@@ -74,10 +74,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_verify_files_sharded_ranks(built, gpu, tmp_path, world):
-    """`world` ranks (all on this box's GPU(s), gloo for the gather) each verify
-    their contiguous shard; the gathered verdicts equal the one-process oracle."""
+@pytest.mark.parametrize("world,backend", [(2, "gloo"), (3, "gloo"), (1, "nccl")])
+def test_verify_files_sharded_ranks(built, gpu, tmp_path, world, backend):
+    """`world` ranks (all on this box's GPU(s)) each verify their contiguous
+    shard; the gathered verdicts equal the one-process oracle.  gloo gathers
+    host tensors (several ranks may share the box's one GPU); the nccl case is
+    RCCL at world size 1 (RCCL refuses two ranks on one GPU): process-group
+    init on the device and the device-tensor all-gather / all-reduce path of
+    shard.py, the one the 8-GPU node runs."""
     pl = 256 * 1024
     sizes = [3, 4 * pl + 17, 2 * pl, 0, 3 * pl - 5, pl + 1, 64, 9 * pl + pl // 2]
     paths, exp = _torrent(tmp_path, pl, sizes, 22)
@@ -89,11 +93,12 @@ def test_verify_files_sharded_ranks(built, gpu, tmp_path, world):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr=127.0.0.1", f"--master-port={_free_port()}",
-           os.path.join(ROOT, "tests", "_reverify_rank.py"), str(spec), str(out), "gloo"]
+           os.path.join(ROOT, "tests", "_reverify_rank.py"), str(spec), str(out), backend]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     res = json.loads(out.read_text())
-    assert res["world"] == world
+    assert res["world"] == world and res["backend"] == backend
+    assert res["gather_ok"]
     assert res["matched"] == want
     n = len(want)
     # pieces overlapping the truncated / missing files

@@ -156,3 +156,13 @@ def test_stats_reverify(built, gpu, tmp_path, pl):
         assert st["pieces_mismatched"] == 1  # I/O errors are counted once, in io_errors
         assert (st["chunk_rounds"] > 0) == (pl >= 1 << 20)
         _check_latency(st)
+        # the call's time budget (vx_tuning_last_verify, recorded per call by bench.py)
+        tr = pool.last_verify()
+        assert tr["read_bytes"] == len(whole)  # every piece byte requested once (failed reads included)
+        assert 0 < tr["read_busy_ms"] and 0 < tr["first_read_ms"] <= tr["wall_ms"] and tr["read_span_ms"] <= tr["wall_ms"]
+        assert 1 <= tr["readers"] <= 16
+        if pl >= 1 << 20:  # chunk rounds: GPU-timed copies of the staged bytes
+            assert tr["rounds"] == st["chunk_rounds"] and tr["copy_bytes"] >= len(whole)
+            assert 0 < tr["copy_busy_ms"] <= tr["copy_span_ms"] + 1e-3 and 0 < tr["copy_busy_frac"] <= 1.0001
+        else:
+            assert tr["rounds"] == 0 and tr["copy_bytes"] == 0

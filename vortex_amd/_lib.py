@@ -39,7 +39,7 @@ EXPORTS = (
     "vx_synth_fill", "vx_sha1_device_uniform_variant", "vx_sha1_device_ragged_variant",
     "vx_tuning_chunk_rounds", "vx_tuning_gather_tiles", "vx_tuning_plan_ragged", "vx_tuning_chunk_schedule",
     "vx_tuning_fail_submit_after", "vx_plan_verify", "vx_get_stats", "vx_reset_stats",
-    "vx_tuning_fail_launch_after",
+    "vx_tuning_fail_launch_after", "vx_tuning_last_verify",
 )
 
 
@@ -75,6 +75,13 @@ class vx_stats(ctypes.Structure):
         "pieces_completed", "pieces_mismatched", "bytes_completed", "batches", "chunk_rounds", "gather_tiles",
         "staged_bytes", "io_errors", "submit_stall_ns", "batch_latency_count", "batch_latency_sum_us",
         "batch_latency_max_us")] + [("batch_latency_hist", ctypes.c_uint64 * VX_STATS_HIST)]
+
+
+class vx_verify_trace(ctypes.Structure):
+    _fields_ = [(name, ctypes.c_double) for name in (
+        "wall_ms", "read_busy_ms", "read_span_ms", "first_read_ms", "copy_busy_ms", "copy_span_ms", "tail_ms")] + [
+        ("read_bytes", ctypes.c_uint64), ("copy_bytes", ctypes.c_uint64), ("readers", ctypes.c_uint32),
+        ("rounds", ctypes.c_uint32)]
 
 
 _lib = None
@@ -122,6 +129,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "vx_tuning_gather_tiles": ([vp], c.c_uint64),
         "vx_tuning_fail_submit_after": ([vp, c.c_int64], None),
         "vx_tuning_fail_launch_after": ([vp, c.c_int64], None),
+        "vx_tuning_last_verify": ([vp, c.POINTER(vx_verify_trace)], c.c_int),
         "vx_plan_verify": ([c.c_uint64, c.c_uint32, c.c_uint64, c.c_uint32, c.c_double, c.POINTER(vx_plan)], c.c_int),
         "vx_tuning_plan_ragged": ([c.c_uint32, c.c_uint32, c.c_uint64], c.c_int),
         "vx_tuning_chunk_schedule": ([c.c_uint64, c.c_uint64, c.c_int, c.c_int, c.POINTER(c.c_uint64), c.c_size_t],

@@ -206,6 +206,10 @@ struct vx_ctx {
     // it (the file re-verify: a piece with an I/O error is counted in
     // io_errors only, FileVerify::consume counts the final verdicts)
     bool harvest_counts_mismatches = true;
+    // vx_tuning_last_verify: the last file re-verify's time budget, and the
+    // timing events around its chunk rounds' data copies (reused across calls)
+    vx_verify_trace last_verify{};
+    std::vector<hipEvent_t> copy_ev;
 };
 
 namespace {
@@ -822,6 +826,8 @@ int vx_destroy(vx_ctx* c) {
     if (c->d_table) (void)hipFree(c->d_table);
     if (c->d_chunk_rows) (void)hipFree(c->d_chunk_rows);
     if (c->chunk_prev) (void)hipEventDestroy(c->chunk_prev);
+    for (hipEvent_t e : c->copy_ev)
+        if (e) (void)hipEventDestroy(e);
     delete c;
     return rc;
 }
@@ -1372,7 +1378,12 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     auto ms = [](clk::time_point a, clk::time_point b) {
         return std::chrono::duration<double, std::milli>(b - a).count();
     };
-    std::vector<hipEvent_t> tev;  // trace: a (start, end) pair per round's data copy
+    // A (start, end) timing-event pair around each round's data copy, kept on
+    // the context and reused (vx_tuning_last_verify; VX_TRACE_ROUNDS prints them).
+    size_t timed = 0;
+    std::vector<uint64_t> timed_bytes;
+    const auto t_last_enqueue_init = clk::now();
+    auto t_last_enqueue = t_last_enqueue_init;
     auto consume = [&] { fv.consume(); };
     // Reserve a slot for round r and queue its reads; false when no slot is
     // free and `block` is not set.
@@ -1423,17 +1434,22 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
         rd.wait(r.ticket);
         const auto t_c = clk::now();
         rc = cp.round(r.si, r.m, r.continues, false, [&](Slot& sl, hipStream_t st) {
-            if (trace) {
-                tev.resize(tev.size() + 2, nullptr);
-                (void)hipEventCreate(&tev[tev.size() - 2]);
-                (void)hipEventCreate(&tev[tev.size() - 1]);
-                (void)hipEventRecord(tev[tev.size() - 2], st);
+            bool ev = true;
+            while (ev && c->copy_ev.size() < 2 * timed + 2) {
+                hipEvent_t e = nullptr;
+                ev = hipEventCreate(&e) == hipSuccess;
+                if (ev) c->copy_ev.push_back(e);
             }
+            ev = ev && hipEventRecord(c->copy_ev[2 * timed], st) == hipSuccess;
             if (hipMemcpyAsync(sl.d_arena, sl.h_stage, sl.bytes, hipMemcpyHostToDevice, st) != hipSuccess)
                 return fail(VX_EDEVICE, "vx_verify_files: chunk H2D failed");
-            if (trace) (void)hipEventRecord(tev.back(), st);
+            if (ev && hipEventRecord(c->copy_ev[2 * timed + 1], st) == hipSuccess) {  // timing is best effort
+                timed_bytes.push_back(sl.bytes);
+                ++timed;
+            }
             return 0;
         });
+        t_last_enqueue = clk::now();
         if (trace)
             std::fprintf(stderr,
                          "vx round %zu slot %d at %.2f: slots+reads %.2f read wait %.2f enqueue %.2f (%zu reading)\n",
@@ -1446,21 +1462,23 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
             sl.state = Slot::FREE;
         }
     rc = cp.finish(fv.matched_out, nullptr, rc, fv.bad.data());
-    if (trace && !tev.empty()) {
-        float t0 = 0, a = 0, b = 0;
-        size_t k = 0;
-        for (const Round& r : rounds) {
-            if (r.m == 0) continue;
-            if (2 * k + 1 >= tev.size()) break;
-            (void)hipEventElapsedTime(&a, tev[0], tev[2 * k]);
-            (void)hipEventElapsedTime(&b, tev[0], tev[2 * k + 1]);
-            std::fprintf(stderr, "vx copy %zu: %.3f -> %.3f ms (%.3f ms, ~%.1f GiB/s) gap %.3f\n", k, a, b, b - a,
-                         r.bytes / ((b - a) * 1e-3) / (1 << 30), a - t0);
+    vx_verify_trace& vt = c->last_verify;
+    vt.tail_ms = ms(t_last_enqueue, clk::now());
+    if (!rc && timed) {  // finish() waited for every round: the copy events are complete
+        float t0 = 0, a = 0, b = 0, busy = 0;
+        for (size_t k = 0; k < timed; ++k) {
+            (void)hipEventElapsedTime(&a, c->copy_ev[0], c->copy_ev[2 * k]);
+            (void)hipEventElapsedTime(&b, c->copy_ev[0], c->copy_ev[2 * k + 1]);
+            busy += b - a;
+            vt.copy_bytes += timed_bytes[k];
+            if (trace)
+                std::fprintf(stderr, "vx copy %zu: %.3f -> %.3f ms (%.3f ms, ~%.1f GiB/s) gap %.3f\n", k, a, b,
+                             b - a, timed_bytes[k] / ((b - a) * 1e-3) / (1 << 30), a - t0);
             t0 = b;
-            ++k;
         }
-        for (hipEvent_t e : tev)
-            if (e) (void)hipEventDestroy(e);
+        vt.copy_busy_ms = busy;
+        vt.copy_span_ms = b;
+        vt.rounds = (uint32_t)timed;
     }
     if (!rc)
         for (uint64_t i = 0; i < cnt; ++i)
@@ -1816,6 +1834,8 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
     if (rc) return rc;
 
     const uint64_t end = first + count;
+    const uint64_t t_call = vx_files::Readers::now_ns();
+    c->last_verify = vx_verify_trace{};
     const std::vector<vx_files::FileSpan> fs = vx_files::layout(file_lengths, nfiles, piece_length);
     std::vector<int> fds(nfiles, -1);
     for (size_t f = 0; f < nfiles; ++f) fds[f] = open(paths[f], O_RDONLY | O_CLOEXEC);
@@ -1838,6 +1858,14 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
             }
         }
         c->harvest_counts_mismatches = true;
+        vx_verify_trace& vt = c->last_verify;
+        vt.read_busy_ms = rd.busy_ns() * 1e-6;
+        vt.read_bytes = rd.bytes_read();
+        vt.readers = (uint32_t)rd.threads();
+        if (rd.first_start_ns()) {
+            vt.read_span_ms = (rd.last_end_ns() - rd.first_start_ns()) * 1e-6;
+            vt.first_read_ms = (rd.first_end_ns() - t_call) * 1e-6;
+        }
         if (rc) {
             // The call fails and its results are dropped: wait for every slot
             // still reading the stages, then free them without harvest(), so
@@ -1854,6 +1882,7 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
     }
     for (int fd : fds)
         if (fd >= 0) close(fd);
+    c->last_verify.wall_ms = (vx_files::Readers::now_ns() - t_call) * 1e-6;
     if (rc) return rc;
     int64_t nbad = 0;
     for (uint8_t x : bad) nbad += x;
@@ -2027,6 +2056,11 @@ int vx_reset_stats(vx_ctx* c) {
 
 uint64_t vx_tuning_chunk_rounds(const vx_ctx* c) { return c ? c->chunk_rounds : 0; }
 uint64_t vx_tuning_gather_tiles(const vx_ctx* c) { return c ? c->gather_tiles : 0; }
+int vx_tuning_last_verify(const vx_ctx* c, vx_verify_trace* out) {
+    if (!c || !out) return fail(VX_EINVAL, "vx_tuning_last_verify: NULL argument");
+    *out = c->last_verify;
+    return 0;
+}
 void vx_tuning_fail_submit_after(vx_ctx* c, int64_t k) {
     if (c) c->fail_submit_after = k < 0 ? -1 : k;
 }

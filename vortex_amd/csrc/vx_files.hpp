@@ -243,6 +243,18 @@ class Readers {
         done_cv_.wait(g, [&] { return jobs_.empty(); });
     }
     void run(const std::vector<ReadItem>& items) { wait(submit(items)); }
+    // Read accounting (vx_tuning_last_verify): pread time summed over threads,
+    // bytes, and the first read's start / the last read's end (steady-clock ns).
+    uint64_t busy_ns() const { return busy_ns_.load(std::memory_order_relaxed); }
+    uint64_t bytes_read() const { return bytes_.load(std::memory_order_relaxed); }
+    uint64_t first_start_ns() const { return first_ns_.load(std::memory_order_relaxed); }
+    uint64_t first_end_ns() const { return first_end_ns_.load(std::memory_order_relaxed); }
+    uint64_t last_end_ns() const { return last_ns_.load(std::memory_order_relaxed); }
+    size_t threads() const { return th_.size(); }
+    static uint64_t now_ns() {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
     // A run builder over this pool's files (whole-piece slots).
     Runs runs(uint64_t max_bytes) const { return Runs(fs_, fds_, pl_, max_bytes); }
     // Kept for the whole-piece path: one job at a time.
@@ -258,6 +270,20 @@ class Readers {
     // wait(), which orders it through mu_.
     void mark_bad(uint64_t piece) { __atomic_store_n(&bad_[piece - first_], (uint8_t)1, __ATOMIC_RELAXED); }
     void read_item(const ReadItem& it, std::vector<Seg>& segs) {
+        const uint64_t t0 = now_ns();
+        uint64_t expect = 0;
+        first_ns_.compare_exchange_strong(expect, t0, std::memory_order_relaxed);
+        read_item_impl(it, segs);
+        const uint64_t t1 = now_ns();
+        busy_ns_.fetch_add(t1 - t0, std::memory_order_relaxed);
+        bytes_.fetch_add(it.len, std::memory_order_relaxed);
+        expect = 0;
+        first_end_ns_.compare_exchange_strong(expect, t1, std::memory_order_relaxed);
+        uint64_t last = last_ns_.load(std::memory_order_relaxed);
+        while (last < t1 && !last_ns_.compare_exchange_weak(last, t1, std::memory_order_relaxed)) {
+        }
+    }
+    void read_item_impl(const ReadItem& it, std::vector<Seg>& segs) {
         if (it.file >= 0 && read_full(fds_[it.file], it.dst, it.file_off, (int64_t)it.len)) return;
         if (it.file < 0) {
             if (!read_range(fs_, fds_, pl_, it, segs)) mark_bad(it.piece);
@@ -310,6 +336,7 @@ class Readers {
     bool stop_ = false, inline_ = false;
     std::deque<Job> jobs_;
     uint64_t base_ = 0;  // id of jobs_.front()
+    std::atomic<uint64_t> busy_ns_{0}, bytes_{0}, first_ns_{0}, first_end_ns_{0}, last_ns_{0};
 };
 
 }  // namespace vx_files

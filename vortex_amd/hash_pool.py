@@ -242,6 +242,21 @@ class HashPool:
     def reset_stats(self) -> None:
         check(lib().vx_reset_stats(self._h), "vx_reset_stats")
 
+    def last_verify(self) -> dict:
+        """Where the last verify_files call spent its time (vx_tuning.h
+        vx_verify_trace), plus the derived rates bench.py records: the
+        readers' pread rate, the data copies' GPU-timed rate, and the fraction
+        of the copy span the copy engine was busy."""
+        t = _lib.vx_verify_trace()
+        check(lib().vx_tuning_last_verify(self._h, ctypes.byref(t)), "vx_tuning_last_verify")
+        d = {name: getattr(t, name) for name, _ in _lib.vx_verify_trace._fields_}
+        gib = float(1 << 30)
+        d["read_GiBps_per_thread"] = t.read_bytes / gib / (t.read_busy_ms * 1e-3) if t.read_busy_ms else None
+        d["read_GiBps"] = t.read_bytes / gib / (t.read_span_ms * 1e-3) if t.read_span_ms else None
+        d["copy_GiBps"] = t.copy_bytes / gib / (t.copy_busy_ms * 1e-3) if t.copy_busy_ms else None
+        d["copy_busy_frac"] = t.copy_busy_ms / t.copy_span_ms if t.copy_span_ms else None
+        return d
+
     # -- bulk verify -----------------------------------------------------------
     def sha1_batch(self, pieces: Sequence) -> list[bytes]:
         n = len(pieces)
