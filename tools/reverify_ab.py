@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""A/B of the config-5 re-verify pipeline, warm and cold.
+
+Writes the linux-mint-geometry file once (fsync'd, on a disk-backed
+filesystem: bench.reverify_dir), then for every engine configuration (env
+knobs read at vx_create) runs `--reps` warm calls and `--cold-reps` calls
+after evicting the file (fsync + POSIX_FADV_DONTNEED), alternating
+configurations per rep so box drift hits all of them alike.  Prints one JSON
+line per configuration with the GiB/s runs and each call's
+vx_tuning_last_verify budget, and the CPU pool on the same file.
+
+usage: python tools/reverify_ab.py [--reps 3] [--cold-reps 2] [--configs name=K=V,K=V;...]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+DEFAULT = "default=;whole=VX_VERIFY_CHUNKED_ABOVE=4194304;ra3=VX_VERIFY_READAHEAD=3;mode3=VX_H2D_MODE=3"
+
+
+def parse(spec):
+    out = []
+    for item in spec.split(";"):
+        name, _, kv = item.partition("=")
+        env = dict(p.split("=", 1) for p in kv.split(",") if p)
+        out.append((name, env))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--cold-reps", type=int, default=2)
+    ap.add_argument("--configs", default=DEFAULT)
+    ap.add_argument("--no-cpu", action="store_true")
+    a = ap.parse_args()
+    import ctypes
+
+    import torch  # noqa: F401  (one HIP runtime)
+
+    import bench
+    import oracle
+    from vortex_amd.hash_pool import HashPool
+
+    pl, total = 2097152, 2907832320
+    n = (total + pl - 1) // pl
+    last = total - (n - 1) * pl
+    threads = bench.cpu_share()
+    d = bench.reverify_dir()
+    path = os.path.join(d, f"vx_ab_linuxmint_{os.getpid()}.iso")
+    buf = ctypes.create_string_buffer(pl)
+    configs = parse(a.configs)
+    res = {name: {"warm": [], "cold": [], "warm_tr": [], "cold_tr": [], "env": env} for name, env in configs}
+    cpu = {"warm": [], "cold": []}
+    try:
+        with open(path, "wb") as f:
+            for i in range(n):
+                L = last if i == n - 1 else pl
+                oracle.lib().vxo_gen_piece(0x5EED0005, i, L, 0, buf)
+                f.write(memoryview(buf)[:L])
+            f.flush()
+            os.fsync(f.fileno())
+        exp = oracle.pool_digest_synth(0x5EED0005, 0, n, pl, last_index=n - 1, last_len=last, threads=threads)
+        pools = {}
+        for name, env in configs:
+            saved = {k: os.environ.get(k) for k in env}
+            os.environ.update(env)
+            pools[name] = HashPool(pl, slots=4, slot_bytes=512 << 20, batch_pieces=4096)
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+            got, bad = pools[name].verify_files([path], [total], pl, exp, io_threads=threads)  # warm-up
+            assert all(got) and bad == 0
+        for leg, reps in (("warm", a.reps), ("cold", a.cold_reps)):
+            for _ in range(reps):
+                for name, _env in configs:
+                    if leg == "cold":
+                        bench.drop_cache(path)
+                    t0 = time.perf_counter()
+                    got, bad = pools[name].verify_files([path], [total], pl, exp, io_threads=threads)
+                    el = time.perf_counter() - t0
+                    assert all(got) and bad == 0
+                    res[name][leg].append(round(total / el / (1 << 30), 2))
+                    tr = pools[name].last_verify()
+                    res[name][leg + "_tr"].append({k: (round(v, 3) if isinstance(v, float) else v)
+                                                   for k, v in tr.items()})
+                    print(f"{leg} {name}: {res[name][leg][-1]} GiB/s", file=sys.stderr, flush=True)
+                if not a.no_cpu:
+                    if leg == "cold":
+                        bench.drop_cache(path)
+                    t0 = time.perf_counter()
+                    ok = oracle.pool_verify_files([path], [total], pl, exp, threads=threads)
+                    cpu[leg].append(round(total / (time.perf_counter() - t0) / (1 << 30), 2))
+                    assert all(ok)
+        for p in pools.values():
+            p.close()
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
+    for name, _ in configs:
+        print(json.dumps({"config": name, **res[name]}))
+    print(json.dumps({"config": "cpu_pool", "threads": threads, **cpu, "dir": d, "fs": bench.fs_type(d)}))
+
+
+if __name__ == "__main__":
+    main()
