@@ -69,12 +69,17 @@ def test_plain_multi_gpu_run_without_gpus_fails_loudly():
 
 
 @pytest.mark.gpu
-def test_plain_bench_launches_its_ranks(built, gpu):
-    r = _run(["--gpus", "2", "--same-device", "--dist-backend", "gloo"] + SMALL, timeout=300)
+@pytest.mark.parametrize("n", [2, 8])
+def test_plain_bench_launches_its_ranks(built, gpu, n):
+    """n = 8 rehearses config 4's shape on the one-GPU box: 8 ranks, global
+    piece indices r*1024 + i, the verdicts of all 8 shards gathered and the
+    exact 1 % mismatch set checked on the gathered table."""
+    r = _run(["--gpus", str(n), "--same-device", "--dist-backend", "gloo"] + SMALL, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     (res,) = _lines(r.stdout)
-    assert res["n_gpus"] == 2 and res["world_size"] == 2 and res["backend"] == "gloo"
+    assert res["n_gpus"] == n and res["world_size"] == n and res["backend"] == "gloo"
     assert res["value"] > 0 and res["config"]["pieces_per_gpu"] == 1024
+    assert res["config"]["total_GiB"] == n * 1024 * 256 / (1 << 20)
 
 
 @pytest.mark.gpu
