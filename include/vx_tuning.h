@@ -62,6 +62,7 @@ typedef struct vx_verify_trace {
     uint64_t copy_bytes;   /* bytes of the timed copies                               */
     uint32_t readers;      /* reader threads                                          */
     uint32_t rounds;       /* timed copies (chunk rounds)                             */
+    uint64_t direct_bytes; /* of read_bytes, read with O_DIRECT (not cached; §6.1)    */
 } vx_verify_trace;
 int vx_tuning_last_verify(const struct vx_ctx* ctx, vx_verify_trace* out);
 

@@ -159,6 +159,9 @@ struct vx_ctx {
     bool verify_overlap = true;  // read round k+1 while round k is enqueued (VX_VERIFY_OVERLAP)
     uint32_t verify_readahead = 2;  // re-verify: rounds / slots read ahead of the enqueue (VX_VERIFY_READAHEAD)
     bool verify_coalesce = true;    // whole-piece re-verify: one pread per run of pieces in one file (VX_VERIFY_COALESCE)
+    // re-verify reads of ranges not in the page cache go O_DIRECT (vx_files::DirectIo;
+    // VX_VERIFY_DIRECT: 0 = never, 1 = when not cached (default), 2 = whenever aligned)
+    int verify_direct = 1;
     uint64_t chunk_rounds = 0;  // chunk rounds launched (vx_tuning_chunk_rounds)
     // Per-piece device rows of the chunk paths (state | expected | digest |
     // verdict), kept across calls and grown on demand: allocating them per
@@ -788,6 +791,7 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (const char* m = std::getenv("VX_VERIFY_OVERLAP")) c->verify_overlap = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_VERIFY_COALESCE")) c->verify_coalesce = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_VERIFY_READAHEAD")) c->verify_readahead = (uint32_t)std::max(1, std::atoi(m));
+    if (const char* m = std::getenv("VX_VERIFY_DIRECT")) c->verify_direct = std::max(0, std::min(2, std::atoi(m)));
     int rc = set_device(c);
     if (!rc && c->h2d_mode == 3 && hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess)
         rc = fail(VX_EDEVICE, "vx_create: copy stream");
@@ -1399,7 +1403,8 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
         Slot& s = c->slots[si];
         reset_fill(s);
         if ((rc = ensure_stage(s))) return false;
-        const uint64_t pitch = align_up(r.len, kAlign);
+        // lanes 4 KiB apart: every stage destination can take an O_DIRECT read
+        const uint64_t pitch = align_up(r.len, vx_files::DirectIo::kBlock);
         auto& it = items[si];
         it.clear();
         uint32_t m = 0;
@@ -1843,7 +1848,8 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
     std::vector<uint8_t> bad(count, 0);
     std::memset(matched_out, 0, count);
     {
-        vx_files::Readers rd(nthreads, fs, fds, piece_length, bad.data(), first);
+        const vx_files::DirectIo dio(paths, fds, c->verify_direct);
+        vx_files::Readers rd(nthreads, fs, fds, piece_length, bad.data(), first, &dio);
         FileVerify fv{c, expected, matched_out, bad};
         c->harvest_counts_mismatches = false;
         rc = chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total, first, end, C)
@@ -1861,6 +1867,7 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
         vx_verify_trace& vt = c->last_verify;
         vt.read_busy_ms = rd.busy_ns() * 1e-6;
         vt.read_bytes = rd.bytes_read();
+        vt.direct_bytes = dio.direct_bytes();
         vt.readers = (uint32_t)rd.threads();
         if (rd.first_start_ns()) {
             vt.read_span_ms = (rd.last_end_ns() - rd.first_start_ns()) * 1e-6;

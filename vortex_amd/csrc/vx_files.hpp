@@ -13,6 +13,8 @@
 // into that slot's pinned stage while the GPU copies and hashes the slots
 // already launched; a piece's segments land back to back at its arena offset.
 #include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -113,16 +115,86 @@ struct ReadItem {
     int64_t file_off = 0;
 };
 
+// Reads that skip the page cache when the data is not in it (DESIGN.md §6.1,
+// round 3).  vortex's re-verify (file_store.rs:271-296) preads through the
+// page cache; at startup the torrent's data is usually not cached, and on the
+// MI355X box a buffered cold pread ran 5-12 GiB/s where O_DIRECT of the same
+// file ran ~20 GiB/s (16 threads, tools/disk_probe.sh, profiles/r03/disk/).
+// Per read: if the first page of the range is not resident (mincore on a
+// PROT_READ mapping of the file, which faults nothing in) and destination,
+// offset and length are 4 KiB aligned, the range goes through an O_DIRECT
+// descriptor; an unaligned tail, a cached range, or a direct read that fails
+// goes through the normal one.  Bytes are the file's either way.
+class DirectIo {
+  public:
+    static constexpr uint64_t kBlock = 4096;  // covers 512 B and 4 KiB logical blocks
+    // mode: 0 = off, 1 = when the range is not cached, 2 = whenever aligned (A/B)
+    DirectIo(const char* const* paths, const std::vector<int>& fds, int mode)
+        : mode_(mode), dfd_(fds.size(), -1), map_(fds.size(), nullptr), size_(fds.size(), 0) {
+        if (mode_ == 0) return;
+        for (size_t f = 0; f < fds.size(); ++f) {
+            struct stat st;
+            if (fds[f] < 0 || fstat(fds[f], &st) != 0 || !S_ISREG(st.st_mode) || st.st_size < (off_t)kBlock) continue;
+            const int d = open(paths[f], O_RDONLY | O_DIRECT | O_CLOEXEC);
+            if (d < 0) continue;  // the filesystem refuses O_DIRECT: buffered reads only
+            void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_SHARED, fds[f], 0);
+            if (m == MAP_FAILED) {
+                close(d);
+                continue;
+            }
+            dfd_[f] = d;
+            map_[f] = m;
+            size_[f] = (uint64_t)st.st_size;
+        }
+    }
+    ~DirectIo() {
+        for (size_t f = 0; f < dfd_.size(); ++f) {
+            if (dfd_[f] >= 0) close(dfd_[f]);
+            if (map_[f]) munmap(map_[f], (size_t)size_[f]);
+        }
+    }
+    DirectIo(const DirectIo&) = delete;
+    DirectIo& operator=(const DirectIo&) = delete;
+
+    // Read [off, off+len) of file f into dst; buffered_fd is the normal descriptor.
+    bool read(uint32_t f, int buffered_fd, uint8_t* dst, int64_t off, int64_t len) const {
+        if (f < dfd_.size() && dfd_[f] >= 0 && len >= (int64_t)kBlock && off >= 0 &&
+            ((reinterpret_cast<uintptr_t>(dst) | (uint64_t)off) & (kBlock - 1)) == 0 &&
+            (uint64_t)(off + len) <= size_[f] && (mode_ == 2 || !resident(f, off))) {
+            const int64_t head = len & ~(int64_t)(kBlock - 1);
+            if (read_full(dfd_[f], dst, off, head)) {
+                direct_bytes_.fetch_add((uint64_t)head, std::memory_order_relaxed);
+                return head == len || read_full(buffered_fd, dst + head, off + head, len - head);
+            }
+        }
+        return read_full(buffered_fd, dst, off, len);
+    }
+    uint64_t direct_bytes() const { return direct_bytes_.load(std::memory_order_relaxed); }
+
+  private:
+    bool resident(uint32_t f, int64_t off) const {
+        unsigned char v = 0;
+        return mincore(static_cast<uint8_t*>(map_[f]) + off, 1, &v) != 0 || (v & 1);  // unknown: stay buffered
+    }
+    const int mode_;
+    std::vector<int> dfd_;
+    std::vector<void*> map_;
+    std::vector<uint64_t> size_;
+    mutable std::atomic<uint64_t> direct_bytes_{0};
+};
+
 // Bytes [start, start+len) of a piece, mapped onto its file segments.
 inline bool read_range(const std::vector<FileSpan>& fs, const std::vector<int>& fds, uint32_t piece_length,
-                       const ReadItem& it, std::vector<Seg>& segs) {
+                       const ReadItem& it, std::vector<Seg>& segs, const DirectIo* dio = nullptr) {
     segments(fs, (int64_t)it.piece, piece_length, segs);
     int64_t pos = 0, at = 0;
     const int64_t a = (int64_t)it.start, b = (int64_t)(it.start + it.len);
     for (const Seg& s : segs) {
         const int64_t lo = std::max<int64_t>(a, pos), hi = std::min<int64_t>(b, pos + s.len);
         if (lo < hi) {
-            if (!read_full(fds[s.file], it.dst + at, s.off + (lo - pos), hi - lo)) return false;
+            const bool ok = dio ? dio->read(s.file, fds[s.file], it.dst + at, s.off + (lo - pos), hi - lo)
+                                : read_full(fds[s.file], it.dst + at, s.off + (lo - pos), hi - lo);
+            if (!ok) return false;
             at += hi - lo;
         }
         pos += s.len;
@@ -191,8 +263,8 @@ class Runs {
 class Readers {
   public:
     Readers(int n, const std::vector<FileSpan>& fs, const std::vector<int>& fds, uint32_t piece_length,
-            uint8_t* bad, uint64_t first = 0)
-        : fs_(fs), fds_(fds), pl_(piece_length), bad_(bad), first_(first) {
+            uint8_t* bad, uint64_t first = 0, const DirectIo* dio = nullptr)
+        : fs_(fs), fds_(fds), pl_(piece_length), bad_(bad), first_(first), dio_(dio) {
         for (int t = 0; t < n; ++t) {
             try {
                 th_.emplace_back([this] { loop(); });
@@ -284,9 +356,13 @@ class Readers {
         }
     }
     void read_item_impl(const ReadItem& it, std::vector<Seg>& segs) {
-        if (it.file >= 0 && read_full(fds_[it.file], it.dst, it.file_off, (int64_t)it.len)) return;
+        if (it.file >= 0) {
+            const bool ok = dio_ ? dio_->read((uint32_t)it.file, fds_[it.file], it.dst, it.file_off, (int64_t)it.len)
+                                 : read_full(fds_[it.file], it.dst, it.file_off, (int64_t)it.len);
+            if (ok) return;
+        }
         if (it.file < 0) {
-            if (!read_range(fs_, fds_, pl_, it, segs)) mark_bad(it.piece);
+            if (!read_range(fs_, fds_, pl_, it, segs, dio_)) mark_bad(it.piece);
             return;
         }
         for (uint32_t k = 0; k < it.pieces; ++k) {  // the run failed: piece by piece, as the walk reads
@@ -330,6 +406,7 @@ class Readers {
     const uint32_t pl_;
     uint8_t* bad_;
     const uint64_t first_;
+    const DirectIo* dio_;
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
