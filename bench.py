@@ -639,13 +639,24 @@ def launch_ranks(args, argv) -> int:
     cmd = launch_cmd(args, argv, _free_port())
     log("launching", args.gpus, "ranks:", " ".join(cmd))
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    import signal
+
+    signal.signal(signal.SIGTERM, lambda *_: sys.exit(143))  # so the handler below runs
     p = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
     lines = []
-    for line in p.stdout:  # stream: a long run keeps printing (stderr is inherited)
-        sys.stdout.write(line)
-        sys.stdout.flush()
-        lines.append(line)
-    rc = p.wait()
+    try:
+        for line in p.stdout:  # stream: a long run keeps printing (stderr is inherited)
+            sys.stdout.write(line)
+            sys.stdout.flush()
+            lines.append(line)
+        rc = p.wait()
+    except BaseException:  # interrupted: take the ranks down with us (the launcher forwards SIGTERM)
+        p.terminate()
+        try:
+            p.wait(timeout=60)
+        except subprocess.TimeoutExpired:
+            p.kill()
+        raise
     if rc != 0:
         log(f"error: the {args.gpus}-rank run failed (rc {rc})")
         return rc

@@ -128,13 +128,20 @@ struct ReadItem {
 class DirectIo {
   public:
     static constexpr uint64_t kBlock = 4096;  // covers 512 B and 4 KiB logical blocks
+    // Files below kMinFile gain nothing (their segments are short and rarely
+    // aligned), and at most kMaxFiles files get a second descriptor and a
+    // mapping, so a torrent of 10^5 small files cannot run the process out of
+    // descriptors or mappings (vm.max_map_count) in the middle of a call.
+    static constexpr uint64_t kMinFile = 1ull << 20;
+    static constexpr size_t kMaxFiles = 4096;
     // mode: 0 = off, 1 = when the range is not cached, 2 = whenever aligned (A/B)
     DirectIo(const char* const* paths, const std::vector<int>& fds, int mode)
         : mode_(mode), dfd_(fds.size(), -1), map_(fds.size(), nullptr), size_(fds.size(), 0) {
         if (mode_ == 0) return;
-        for (size_t f = 0; f < fds.size(); ++f) {
+        size_t used = 0;
+        for (size_t f = 0; f < fds.size() && used < kMaxFiles; ++f) {
             struct stat st;
-            if (fds[f] < 0 || fstat(fds[f], &st) != 0 || !S_ISREG(st.st_mode) || st.st_size < (off_t)kBlock) continue;
+            if (fds[f] < 0 || fstat(fds[f], &st) != 0 || !S_ISREG(st.st_mode) || st.st_size < (off_t)kMinFile) continue;
             const int d = open(paths[f], O_RDONLY | O_DIRECT | O_CLOEXEC);
             if (d < 0) continue;  // the filesystem refuses O_DIRECT: buffered reads only
             void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_SHARED, fds[f], 0);
@@ -145,6 +152,7 @@ class DirectIo {
             dfd_[f] = d;
             map_[f] = m;
             size_[f] = (uint64_t)st.st_size;
+            ++used;
         }
     }
     ~DirectIo() {
