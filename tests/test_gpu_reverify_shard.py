@@ -159,3 +159,55 @@ def test_verify_files_multi_contexts(built, gpu, tmp_path, nctx, pl):
     finally:
         for p in pools:
             p.close()
+
+
+@pytest.mark.parametrize("pl", [256 * 1024, 2 << 20])  # whole-piece slots / resumable chunk rounds
+def test_verify_files_cold_direct_reads(built, gpu, tmp_path, pl):
+    """Re-verify of files whose pages are NOT in the page cache: the readers
+    take the O_DIRECT path for aligned, uncached ranges (vx_files::DirectIo,
+    DESIGN.md §6.1) and the buffered path for the rest (unaligned segments
+    where files meet, a short tail).  Verdicts equal the oracle's on the same
+    damaged multi-file torrent, and the call's trace shows direct reads when
+    the filesystem takes O_DIRECT."""
+    from vortex_amd.hash_pool import HashPool
+
+    d = str(tmp_path)
+    try:
+        fd = os.open(os.path.join(d, "probe"), os.O_CREAT | os.O_RDWR | os.O_DIRECT, 0o600)
+        os.close(fd)
+        direct_ok = True
+    except OSError:
+        direct_ok = False
+    sizes = [3 * pl + 4096 * 3, 5 * pl, 2 * pl + 777, pl + 1, 9 * pl]  # aligned and misaligned file starts
+    paths, exp = _torrent(tmp_path, pl, sizes, 31)
+    with open(paths[1], "r+b") as f:  # one flipped byte in an aligned region
+        f.seek(2 * pl + 5000)
+        b = f.read(1)
+        f.seek(2 * pl + 5000)
+        f.write(bytes([b[0] ^ 0x11]))
+    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
+    assert not all(want) and any(want)
+
+    def evict():
+        for p in paths:
+            fd = os.open(p, os.O_RDONLY)
+            os.fsync(fd)
+            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+            os.close(fd)
+
+    with HashPool(pl, slots=3, slot_bytes=16 << 20) as pool:
+        for _ in range(2):
+            evict()
+            got, bad = pool.verify_files(paths, sizes, pl, exp, io_threads=4)
+            assert got == want and bad == 0
+            tr = pool.last_verify()
+            assert tr["read_bytes"] == sum(sizes)
+            if direct_ok:
+                assert tr["direct_bytes"] > 0
+        # cached now (the buffered reads above filled part of it; read the rest): no direct reads
+        for p in paths:
+            with open(p, "rb") as f:
+                while f.read(1 << 20):
+                    pass
+        got, bad = pool.verify_files(paths, sizes, pl, exp, io_threads=4)
+        assert got == want and pool.last_verify()["direct_bytes"] == 0
