@@ -1386,8 +1386,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     // the context and reused (vx_tuning_last_verify; VX_TRACE_ROUNDS prints them).
     size_t timed = 0;
     std::vector<uint64_t> timed_bytes;
-    const auto t_last_enqueue_init = clk::now();
-    auto t_last_enqueue = t_last_enqueue_init;
+    auto t_last_enqueue = clk::now();
     auto consume = [&] { fv.consume(); };
     // Reserve a slot for round r and queue its reads; false when no slot is
     // free and `block` is not set.
