@@ -6,7 +6,13 @@ flipped bytes, truncated and missing files, random piece ranges; every
 call is compared with the CPU restatement oracle.pool_verify_files (test
 infrastructure).  Any difference exits non-zero.  Prints one JSON line.
 
-usage: python tools/soak_files.py [--seconds 60] [--seed 1] [--dir /tmp]
+With --cold, every call first evicts the torrent's files from the page cache
+(fsync + POSIX_FADV_DONTNEED), so the readers take their O_DIRECT path for
+aligned uncached ranges (vx_files::DirectIo) and the buffered one for the
+rest; the bytes read direct are summed in the JSON.  Without --dir, the soak
+runs in the first disk-backed directory (bench.reverify_dir).
+
+usage: python tools/soak_files.py [--seconds 60] [--seed 1] [--dir DIR] [--cold]
 """
 import argparse
 import hashlib
@@ -26,20 +32,32 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--seconds", type=float, default=60)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--dir", default=os.environ.get("TMPDIR", "/tmp"))
+    ap.add_argument("--dir", default=None)
+    ap.add_argument("--cold", action="store_true", help="evict the files before every call")
     a = ap.parse_args()
+    import bench
     import oracle
     from vortex_amd.hash_pool import HashPool
 
+    if a.dir is None:
+        a.dir = bench.reverify_dir()
     rng = random.Random(a.seed)
     t_end = time.time() + a.seconds
-    stats = {"torrents": 0, "calls": 0, "pieces": 0, "bad_pieces": 0}
+    stats = {"torrents": 0, "calls": 0, "pieces": 0, "bad_pieces": 0, "direct_bytes": 0, "read_bytes": 0}
+
+    def evict(paths):
+        if not a.cold:
+            return
+        for p in paths:
+            if os.path.exists(p):
+                bench.drop_cache(p)
     root = tempfile.mkdtemp(prefix="vx_soak_files_", dir=a.dir)
     try:
         while time.time() < t_end:
             pl = rng.choice([16384, 65536, 262144, 300000, (1 << 20) + 3072, 2 << 20, 4 << 20])
             nfiles = rng.randint(1, 10)
-            sizes = [rng.choice([0, rng.randint(1, 4 * pl), rng.randint(1, 200), rng.randint(pl, 6 * pl)])
+            sizes = [rng.choice([0, rng.randint(1, 4 * pl), rng.randint(1, 200), rng.randint(pl, 6 * pl),
+                                 rng.randint(1, 6) * pl, rng.randint(256, 2048) * 4096])
                      for _ in range(nfiles)]
             if sum(sizes) == 0:
                 sizes[0] = pl + 1
@@ -77,13 +95,18 @@ def main():
             slots = rng.choice([2, 3, 4])
             slot_bytes = max(pl, rng.choice([4 << 20, 32 << 20, 256 << 20]))
             with HashPool(pl, slots=slots, batch_pieces=rng.choice([4, 64, 4096]), slot_bytes=slot_bytes) as pool:
+                evict(paths)
                 got, bad = pool.verify_files(paths, sizes, pl, exp, io_threads=rng.choice([0, 1, 3, 8]))
+                tr = pool.last_verify()
+                stats["direct_bytes"] += tr["direct_bytes"]
+                stats["read_bytes"] += tr["read_bytes"]
                 stats["calls"] += 1
                 if got != want:
                     print(json.dumps({"error": "verdicts differ", "pl": pl, "sizes": sizes}))
                     return 1
                 first = rng.randrange(n)
                 count = rng.randint(0, n - first)
+                evict(paths)
                 sub, _ = pool.verify_files(paths, sizes, pl, exp, io_threads=2, first=first, count=count)
                 stats["calls"] += 1
                 if sub != want[first:first + count]:
