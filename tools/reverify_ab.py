@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--cold-reps", type=int, default=2)
     ap.add_argument("--configs", default=DEFAULT)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cold-only", action="store_true")
     a = ap.parse_args()
     import ctypes
 
@@ -106,7 +107,15 @@ def main():
             os.unlink(path)
     for name, _ in configs:
         print(json.dumps({"config": name, **res[name]}))
-    print(json.dumps({"config": "cpu_pool", "threads": threads, **cpu, "dir": d, "fs": bench.fs_type(d)}))
+    node = None
+    try:
+        pr = torch.cuda.get_device_properties(0)
+        bus = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        node = open(f"/sys/bus/pci/devices/{bus}/numa_node").read().strip()
+    except Exception as e:  # noqa: BLE001  (diagnostic only)
+        node = f"? ({e})"
+    print(json.dumps({"config": "cpu_pool", "threads": threads, **cpu, "dir": d, "fs": bench.fs_type(d),
+                      "gpu_numa_node": node}))
 
 
 if __name__ == "__main__":

@@ -29,6 +29,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
 #include <chrono>
 #include <cmath>
 #include <cstdlib>
@@ -162,6 +163,9 @@ struct vx_ctx {
     // re-verify reads of ranges not in the page cache go O_DIRECT (vx_files::DirectIo;
     // VX_VERIFY_DIRECT: 0 = never, 1 = when not cached (default), 2 = whenever aligned)
     int verify_direct = 1;
+    // re-verify reader threads pinned to the CPUs of the GPU's NUMA node
+    // (VX_VERIFY_NUMA=1; gpu_numa_cpus) — A/B, off by default
+    int verify_numa = 0;
     uint64_t chunk_rounds = 0;  // chunk rounds launched (vx_tuning_chunk_rounds)
     // Per-piece device rows of the chunk paths (state | expected | digest |
     // verdict), kept across calls and grown on demand: allocating them per
@@ -792,6 +796,7 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (const char* m = std::getenv("VX_VERIFY_COALESCE")) c->verify_coalesce = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_VERIFY_READAHEAD")) c->verify_readahead = (uint32_t)std::max(1, std::atoi(m));
     if (const char* m = std::getenv("VX_VERIFY_DIRECT")) c->verify_direct = std::max(0, std::min(2, std::atoi(m)));
+    if (const char* m = std::getenv("VX_VERIFY_NUMA")) c->verify_numa = std::atoi(m) != 0;
     int rc = set_device(c);
     if (!rc && c->h2d_mode == 3 && hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess)
         rc = fail(VX_EDEVICE, "vx_create: copy stream");
@@ -1018,6 +1023,49 @@ struct FileVerify {
         }
     }
 };
+
+// The CPUs of the NUMA node the context's GPU hangs off (sysfs numa_node of
+// its PCI function, then that node's cpulist), intersected with this
+// process's affinity.  false when any step is unavailable or the
+// intersection is empty.
+bool gpu_numa_cpus(const vx_ctx* c, cpu_set_t* out) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), c->cfg.device) != hipSuccess) return false;
+    for (char* p = bus; *p; ++p) *p = (char)std::tolower((unsigned char)*p);
+    auto read_line = [](const std::string& path) {
+        std::string v;
+        if (FILE* f = std::fopen(path.c_str(), "r")) {
+            char buf[4096];
+            if (std::fgets(buf, sizeof(buf), f)) v = buf;
+            std::fclose(f);
+        }
+        return v;
+    };
+    const std::string node = read_line(std::string("/sys/bus/pci/devices/") + bus + "/numa_node");
+    if (node.empty() || node[0] == '-') return false;
+    const std::string list = read_line("/sys/devices/system/node/node" + std::to_string(std::atoi(node.c_str())) +
+                                       "/cpulist");
+    cpu_set_t mine;
+    if (list.empty() || sched_getaffinity(0, sizeof(mine), &mine) != 0) return false;
+    CPU_ZERO(out);
+    size_t at = 0;
+    while (at < list.size()) {  // "0-63,128-191\n"
+        char* end = nullptr;
+        const long a = std::strtol(list.c_str() + at, &end, 10);
+        if (end == list.c_str() + at) break;
+        long b = a;
+        at = (size_t)(end - list.c_str());
+        if (at < list.size() && list[at] == '-') {
+            b = std::strtol(list.c_str() + at + 1, &end, 10);
+            at = (size_t)(end - list.c_str());
+        }
+        for (long k = a; k <= b && k < CPU_SETSIZE; ++k)
+            if (k >= 0 && CPU_ISSET(k, &mine)) CPU_SET(k, out);
+        if (at < list.size() && list[at] == ',') ++at;
+        else break;
+    }
+    return CPU_COUNT(out) > 0;
+}
 
 // Re-verify chunk size for `count` pieces: 256 KiB when
 // every piece's chunk fits one slot arena (a single window of rounds), else
@@ -1848,7 +1896,9 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
     std::memset(matched_out, 0, count);
     {
         const vx_files::DirectIo dio(paths, fds, c->verify_direct);
-        vx_files::Readers rd(nthreads, fs, fds, piece_length, bad.data(), first, &dio);
+        cpu_set_t numa;
+        const bool pin = c->verify_numa && gpu_numa_cpus(c, &numa);
+        vx_files::Readers rd(nthreads, fs, fds, piece_length, bad.data(), first, &dio, pin ? &numa : nullptr);
         FileVerify fv{c, expected, matched_out, bad};
         c->harvest_counts_mismatches = false;
         rc = chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total, first, end, C)

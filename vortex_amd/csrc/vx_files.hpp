@@ -13,6 +13,8 @@
 // into that slot's pinned stage while the GPU copies and hashes the slots
 // already launched; a piece's segments land back to back at its arena offset.
 #include <fcntl.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -270,12 +272,21 @@ class Runs {
 // is the first piece of the verified range.
 class Readers {
   public:
+    // cpus (may be NULL): pin every reader thread to this set (the GPU's NUMA
+    // node, vx_engine.hip gpu_numa_cpus); pinning is best effort.
     Readers(int n, const std::vector<FileSpan>& fs, const std::vector<int>& fds, uint32_t piece_length,
-            uint8_t* bad, uint64_t first = 0, const DirectIo* dio = nullptr)
+            uint8_t* bad, uint64_t first = 0, const DirectIo* dio = nullptr, const cpu_set_t* cpus = nullptr)
         : fs_(fs), fds_(fds), pl_(piece_length), bad_(bad), first_(first), dio_(dio) {
+        if (cpus) {
+            cpus_ = *cpus;
+            pin_ = true;
+        }
         for (int t = 0; t < n; ++t) {
             try {
-                th_.emplace_back([this] { loop(); });
+                th_.emplace_back([this] {
+                    if (pin_) (void)pthread_setaffinity_np(pthread_self(), sizeof(cpus_), &cpus_);
+                    loop();
+                });
             } catch (...) {  // no more threads: the ones already started do the reads
                 break;
             }
@@ -415,6 +426,8 @@ class Readers {
     uint8_t* bad_;
     const uint64_t first_;
     const DirectIo* dio_;
+    cpu_set_t cpus_{};
+    bool pin_ = false;
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;
