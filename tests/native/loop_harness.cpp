@@ -19,23 +19,43 @@
 // a configurable fraction of first deliveries is corrupted, so the mismatch
 // branch runs and the piece is downloaded again.
 //
+// Faults (INTEGRATION.md "One ownership rule for submits" / "Device
+// failure"): with fail_submit_every = K > 0 every K-th submit is refused
+// (vx_tuning_fail_submit_after, non-sticky VX_ENOMEM), and with
+// fail_launch_after = L >= 0 the (L+1)-th batch launch fails like a device
+// error.  The harness then does what INTEGRATION.md's Rust call sites do: a
+// refused piece goes to "vortex's own pool" (a small thread pool running the
+// CPU restatement of the sha1 closure, oracle/liboracle.so, with results over
+// a channel drained each turn); after the device fails, vx_poll is drained
+// until it errors, vx_destroy waits for the device, every still-inflight piece
+// goes to the CPU pool, and every later piece is hashed there.  Every delivery
+// must produce exactly one verdict.
+//
 // usage: loop_harness <expected.bin> <n_pieces> <piece_len> <last_len> <seed>
 //                     [peers=32] [subpieces_per_turn=4] [corrupt_every=50]
+//                     [fail_submit_every=0] [fail_launch_after=-1]
 // prints one JSON line; exit status 0 iff every piece completed with the
 // expected digest and every corrupted delivery was rejected.
 #include <sys/mman.h>
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <mutex>
+#include <thread>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "vx_hash.h"
+#include "vx_tuning.h"
+
+extern "C" void vxo_sha1(const uint8_t* data, size_t len, uint8_t out[20]);  // oracle/liboracle.so
 
 namespace {
 
@@ -64,6 +84,76 @@ double now_ms() {
     return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// vortex's own pool for pieces the GPU does not take: the reference's closure
+// (peer_connection.rs:1145-1158) on worker threads, results over a channel
+// (the downloaded_piece_tx/rc pair, torrent.rs:319-320) drained by the loop.
+class CpuPool {
+  public:
+    struct Done {
+        uint64_t tag;
+        bool matched;
+    };
+    explicit CpuPool(int threads) {
+        for (int t = 0; t < threads; ++t) th_.emplace_back([this] { run(); });
+    }
+    ~CpuPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void spawn(uint64_t tag, const uint8_t* buf, uint32_t len, const uint8_t* expected) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            q_.push_back(Job{tag, buf, len, expected});
+        }
+        cv_.notify_one();
+    }
+    void try_recv(std::vector<Done>& out) {
+        std::lock_guard<std::mutex> g(mu_);
+        out.insert(out.end(), done_.begin(), done_.end());
+        done_.clear();
+    }
+    bool idle() {
+        std::lock_guard<std::mutex> g(mu_);
+        return q_.empty() && busy_ == 0;
+    }
+
+  private:
+    struct Job {
+        uint64_t tag;
+        const uint8_t* buf;
+        uint32_t len;
+        const uint8_t* expected;
+    };
+    void run() {
+        std::unique_lock<std::mutex> g(mu_);
+        for (;;) {
+            cv_.wait(g, [&] { return stop_ || !q_.empty(); });
+            if (q_.empty()) return;
+            const Job j = q_.front();
+            q_.pop_front();
+            ++busy_;
+            g.unlock();
+            uint8_t d[20];
+            vxo_sha1(j.buf, j.len, d);
+            const bool m = std::memcmp(d, j.expected, 20) == 0;
+            g.lock();
+            --busy_;
+            done_.push_back(Done{j.tag, m});
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<Job> q_;
+    std::vector<Done> done_;
+    int busy_ = 0;
+    bool stop_ = false;
+};
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -80,6 +170,8 @@ int main(int argc, char** argv) {
     const uint32_t peers = argc > 6 ? (uint32_t)std::atoi(argv[6]) : 32;
     const uint32_t subs_per_turn = argc > 7 ? (uint32_t)std::atoi(argv[7]) : 4;
     const uint32_t corrupt_every = argc > 8 ? (uint32_t)std::atoi(argv[8]) : 50;
+    const uint32_t fail_submit_every = argc > 9 ? (uint32_t)std::atoi(argv[9]) : 0;
+    const int64_t fail_launch_after = argc > 10 ? std::atoll(argv[10]) : -1;
 
     std::vector<uint8_t> expected((size_t)n * 20);
     FILE* f = std::fopen(exp_path, "rb");
@@ -112,6 +204,11 @@ int main(int argc, char** argv) {
     }
     std::vector<uint32_t> free_bufs;
     for (uint32_t b = 0; b < nbuf; ++b) free_bufs.push_back(nbuf - 1 - b);
+    if (fail_launch_after >= 0) vx_tuning_fail_launch_after(ctx, fail_launch_after);
+    CpuPool cpu(4);
+    std::unordered_set<uint64_t> on_cpu;  // tags handed to the CPU pool
+    bool gpu_dead = false;
+    uint64_t refused = 0, cpu_hashed = 0, recovered = 0, submits = 0;
 
     struct Download {
         uint32_t piece, buf, next_sub, nsub, len;
@@ -152,9 +249,23 @@ int main(int argc, char** argv) {
             if (d.next_sub == d.nsub) {  // complete → hash (peer_connection.rs:1145)
                 const uint64_t tag = (tag_seq++ << 32) | d.piece;
                 const uint8_t* buf = pool[d.buf];
-                if (int rc = vx_submit(ctx, tag, buf, d.len, &expected[(size_t)d.piece * 20])) {
-                    std::fprintf(stderr, "vx_submit: %d %s\n", rc, vx_last_error());
-                    return 1;
+                const uint8_t* want = &expected[(size_t)d.piece * 20];
+                int rc = VX_EDEVICE;
+                if (!gpu_dead) {
+                    if (fail_submit_every && ++submits % fail_submit_every == 0) vx_tuning_fail_submit_after(ctx, 0);
+                    rc = vx_submit(ctx, tag, buf, d.len, want);
+                }
+                if (rc != 0) {
+                    // not taken (vx_hash.h ownership rule): the reference's closure runs on the CPU pool
+                    if (rc != VX_ENOMEM && rc != VX_EDEVICE) {
+                        std::fprintf(stderr, "vx_submit: %d %s\n", rc, vx_last_error());
+                        return 1;
+                    }
+                    if (!gpu_dead) ++refused;
+                    if (rc == VX_EDEVICE) gpu_dead = true;
+                    cpu.spawn(tag, buf, d.len, want);
+                    on_cpu.insert(tag);
+                    ++cpu_hashed;
                 }
                 inflight[tag] = {d.buf, now_ms()};
                 bytes += d.len;
@@ -165,49 +276,89 @@ int main(int argc, char** argv) {
             }
         }
         // end of loop turn: drain completions (event_loop.rs:554-557)
-        if (int rc = vx_flush(ctx)) {
-            std::fprintf(stderr, "vx_flush: %d\n", rc);
-            return 1;
-        }
-        for (;;) {
-            const int64_t k = vx_poll(ctx, cq.data(), cq.size());
-            if (k < 0) {
-                std::fprintf(stderr, "vx_poll: %lld %s\n", (long long)k, vx_last_error());
-                return 1;
+        auto verdict = [&](uint64_t tag, bool matched) -> bool {
+            const uint32_t p = (uint32_t)(tag & 0xFFFFFFFFu);
+            auto it = inflight.find(tag);
+            if (it == inflight.end()) return false;  // unknown or duplicate: exactly-once broken
+            lat.push_back(now_ms() - it->second.second);
+            free_bufs.push_back(it->second.first);  // return_buffer
+            inflight.erase(it);
+            ++hashed;
+            const bool was_corrupt = corrupt_every && attempts[p] == 1 && p % corrupt_every == corrupt_every / 2;
+            if (matched) {
+                if (was_corrupt) ++wrong;  // corrupted data must never verify
+                complete[p] = 1;
+                ++done_count;
+            } else {
+                if (!was_corrupt) ++wrong;  // clean data must always verify
+                ++rejected;
+                todo.push_back(p);  // mark_not_downloaded → re-request
             }
-            for (int64_t j = 0; j < k; ++j) {
-                const vx_completion& c = cq[j];
-                const uint32_t p = (uint32_t)(c.tag & 0xFFFFFFFFu);
-                auto it = inflight.find(c.tag);
-                if (it == inflight.end()) return 1;
-                lat.push_back(now_ms() - it->second.second);
-                free_bufs.push_back(it->second.first);  // return_buffer
-                inflight.erase(it);
-                ++hashed;
-                const bool was_corrupt = corrupt_every && attempts[p] == 1 && p % corrupt_every == corrupt_every / 2;
-                if (c.matched) {
-                    if (was_corrupt) ++wrong;  // corrupted data must never verify
-                    complete[p] = 1;
-                    ++done_count;
-                } else {
-                    if (!was_corrupt) ++wrong;  // clean data must always verify
-                    ++rejected;
-                    todo.push_back(p);  // mark_not_downloaded → re-request
+            return true;
+        };
+        bool failed_now = false;
+        if (ctx) {
+            if (vx_flush(ctx) != 0) failed_now = true;
+            for (;;) {
+                const int64_t k = vx_poll(ctx, cq.data(), cq.size());
+                if (k < 0) {
+                    failed_now = true;
+                    break;
                 }
+                for (int64_t j = 0; j < k; ++j)
+                    if (!verdict(cq[j].tag, cq[j].matched != 0)) return 4;
+                if ((size_t)k < cq.size()) break;
             }
-            if ((size_t)k < cq.size()) break;
         }
+        if (failed_now) {
+            // device failure: vx_poll has handed out every
+            // finished result; vx_destroy waits for the device, then every
+            // piece still with the GPU is hashed on the CPU pool.
+            for (;;) {  // drain what is left after a flush-time error
+                const int64_t k = vx_poll(ctx, cq.data(), cq.size());
+                if (k <= 0) break;
+                for (int64_t j = 0; j < k; ++j)
+                    if (!verdict(cq[j].tag, cq[j].matched != 0)) return 4;
+            }
+            const uint64_t pending = vx_pending(ctx);
+            vx_destroy(ctx);  // waits for the device, unregisters the pool buffers
+            ctx = nullptr;
+            gpu_dead = true;
+            // the GPU's unfinished pieces (take_unfinished): every inflight tag not already on the CPU pool
+            uint64_t handed = 0;
+            for (const auto& kv : inflight) {
+                const uint64_t t = kv.first;
+                if (on_cpu.count(t)) continue;
+                const uint32_t p = (uint32_t)(t & 0xFFFFFFFFu);
+                cpu.spawn(t, pool[kv.second.first], p == n - 1 ? last_len : plen, &expected[(size_t)p * 20]);
+                on_cpu.insert(t);
+                ++handed;
+            }
+            recovered += handed;
+            if (handed != pending) {
+                std::fprintf(stderr, "unfinished %llu != vx_pending %llu\n", (unsigned long long)handed,
+                             (unsigned long long)pending);
+                return 5;
+            }
+        }
+        std::vector<CpuPool::Done> cdone;
+        cpu.try_recv(cdone);
+        for (const auto& d : cdone)
+            if (!verdict(d.tag, d.matched)) return 4;
         if (active.empty() && todo.empty() && !inflight.empty()) {
             // nothing left to receive: block for the GPU like the loop's
             // CQE wait would (torrent.rs:42, event_loop.rs:438-439)
-            vx_drain(ctx, 0);
+            if (ctx) vx_drain(ctx, 0);
+            else std::this_thread::sleep_for(std::chrono::microseconds(200));
         }
     }
     const double el = now_ms() - t0;
     vx_stats st{};  // what the event loop would export under vortex's `metrics` feature
-    vx_get_stats(ctx, &st);
-    for (uint8_t* b : pool) vx_unregister_host_buffer(ctx, b);
-    vx_destroy(ctx);
+    if (ctx) {
+        vx_get_stats(ctx, &st);
+        for (uint8_t* b : pool) vx_unregister_host_buffer(ctx, b);
+        vx_destroy(ctx);
+    }
     for (uint8_t* b : pool) munmap(b, plen);
     std::sort(lat.begin(), lat.end());
     auto pct = [&](double q) { return lat.empty() ? 0.0 : lat[std::min(lat.size() - 1, (size_t)(q * lat.size()))]; };
@@ -215,11 +366,13 @@ int main(int argc, char** argv) {
         "{\"pieces\": %u, \"piece_len\": %u, \"hashed\": %llu, \"rejected\": %llu, \"wrong\": %llu, \"turns\": %llu, "
         "\"elapsed_ms\": %.1f, \"GiBps\": %.3f, \"latency_ms_p50\": %.2f, \"latency_ms_p99\": %.2f, "
         "\"latency_ms_max\": %.2f, \"engine\": {\"pieces_completed\": %llu, \"pieces_mismatched\": %llu, "
-        "\"bytes_completed\": %llu, \"batches\": %llu, \"submit_stall_ms\": %.3f, \"batch_latency_max_ms\": %.3f}}\n",
+        "\"bytes_completed\": %llu, \"batches\": %llu, \"submit_stall_ms\": %.3f, \"batch_latency_max_ms\": %.3f}, "
+        "\"faults\": {\"refused\": %llu, \"cpu_hashed\": %llu, \"recovered\": %llu, \"gpu_dead\": %d}}\n",
         n, plen, (unsigned long long)hashed, (unsigned long long)rejected, (unsigned long long)wrong,
         (unsigned long long)turns, el, bytes / (el * 1e-3) / (1 << 30), pct(0.5), pct(0.99), lat.empty() ? 0 : lat.back(),
         (unsigned long long)st.pieces_completed, (unsigned long long)st.pieces_mismatched,
         (unsigned long long)st.bytes_completed, (unsigned long long)st.batches, st.submit_stall_ns * 1e-6,
-        st.batch_latency_max_us * 1e-3);
+        st.batch_latency_max_us * 1e-3, (unsigned long long)refused, (unsigned long long)(cpu_hashed + recovered),
+        (unsigned long long)recovered, gpu_dead ? 1 : 0);
     return wrong == 0 && done_count == n ? 0 : 3;
 }
