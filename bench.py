@@ -420,7 +420,7 @@ def reverify_dir() -> str:
     return next(d for d in cands if d and os.path.isdir(d) and os.access(d, os.W_OK))
 
 
-def reverify_leg(reps: int = 3, cold_reps: int = 3):
+def reverify_leg(reps: int = 5, cold_reps: int = 3):
     """BASELINE config 5: full re-verify of a torrent's data from disk with
     the linux-mint geometry (cli/linux-mint.torrent: 2,907,832,320 B, 2 MiB
     pieces, last 1,179,648 B) through vx_verify_files (pread into pinned
