@@ -114,8 +114,8 @@ def _disk_dir(tmp_path):
 def test_direct_reads_of_uncached_ranges(tmp_path):
     """vx_files::DirectIo (the re-verify's O_DIRECT path, DESIGN.md §6.1):
     every read returns the file's bytes whatever the alignment; ranges not in
-    the page cache go O_DIRECT (mode 1) and cached ones do not; mode 0 never,
-    mode 2 whenever aligned."""
+    the page cache go O_DIRECT (mode 1: mincore probe; mode 3: RWF_NOWAIT
+    read first) and cached ones do not; mode 0 never, mode 2 whenever aligned."""
     d = _disk_dir(tmp_path)
     if d is None:
         pytest.skip("no filesystem here takes O_DIRECT")
@@ -151,6 +151,9 @@ def test_direct_reads_of_uncached_ranges(tmp_path):
         assert forced > 0
         # evicted pages read direct (the kernel may keep a few pages; most ranges go direct)
         assert cold > 0
+        # mode 3: RWF_NOWAIT from the page cache, O_DIRECT for what it could not return
+        assert run(3, evict=False) == 0
+        assert run(3, evict=True) > 0
     finally:
         if os.path.exists(path):
             os.unlink(path)

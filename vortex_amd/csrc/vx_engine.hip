@@ -795,7 +795,7 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (const char* m = std::getenv("VX_VERIFY_OVERLAP")) c->verify_overlap = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_VERIFY_COALESCE")) c->verify_coalesce = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_VERIFY_READAHEAD")) c->verify_readahead = (uint32_t)std::max(1, std::atoi(m));
-    if (const char* m = std::getenv("VX_VERIFY_DIRECT")) c->verify_direct = std::max(0, std::min(2, std::atoi(m)));
+    if (const char* m = std::getenv("VX_VERIFY_DIRECT")) c->verify_direct = std::max(0, std::min(3, std::atoi(m)));
     if (const char* m = std::getenv("VX_VERIFY_NUMA")) c->verify_numa = std::atoi(m) != 0;
     int rc = set_device(c);
     if (!rc && c->h2d_mode == 3 && hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess)

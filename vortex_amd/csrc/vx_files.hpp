@@ -17,7 +17,10 @@
 #include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/uio.h>
 #include <unistd.h>
+
+#include <cerrno>
 
 #include <algorithm>
 #include <atomic>
@@ -136,7 +139,9 @@ class DirectIo {
     // descriptors or mappings (vm.max_map_count) in the middle of a call.
     static constexpr uint64_t kMinFile = 1ull << 20;
     static constexpr size_t kMaxFiles = 4096;
-    // mode: 0 = off, 1 = when the range is not cached, 2 = whenever aligned (A/B)
+    // mode: 0 = off, 1 = when the range's first page is not cached (mincore),
+    // 2 = whenever aligned (A/B), 3 = read from the page cache without waiting
+    // (preadv2 RWF_NOWAIT) and O_DIRECT whatever it could not return (A/B)
     DirectIo(const char* const* paths, const std::vector<int>& fds, int mode)
         : mode_(mode), dfd_(fds.size(), -1), map_(fds.size(), nullptr), size_(fds.size(), 0) {
         if (mode_ == 0) return;
@@ -168,9 +173,36 @@ class DirectIo {
 
     // Read [off, off+len) of file f into dst; buffered_fd is the normal descriptor.
     bool read(uint32_t f, int buffered_fd, uint8_t* dst, int64_t off, int64_t len) const {
-        if (f < dfd_.size() && dfd_[f] >= 0 && len >= (int64_t)kBlock && off >= 0 &&
-            ((reinterpret_cast<uintptr_t>(dst) | (uint64_t)off) & (kBlock - 1)) == 0 &&
-            (uint64_t)(off + len) <= size_[f] && (mode_ == 2 || !resident(f, off))) {
+        const bool aligned = f < dfd_.size() && dfd_[f] >= 0 && len >= (int64_t)kBlock && off >= 0 &&
+                             ((reinterpret_cast<uintptr_t>(dst) | (uint64_t)off) & (kBlock - 1)) == 0 &&
+                             (uint64_t)(off + len) <= size_[f];
+        if (aligned && mode_ == 3 && !nowait_unsupported_.load(std::memory_order_relaxed)) {
+            // Whatever the page cache holds comes back at once; the read stops
+            // at the first page that would need the disk.
+            int64_t got = 0;
+            while (got < len) {
+                struct iovec v{dst + got, (size_t)(len - got)};
+                const ssize_t r = preadv2(buffered_fd, &v, 1, (off_t)(off + got), RWF_NOWAIT);
+                if (r > 0) {
+                    got += r;
+                    continue;
+                }
+                if (r < 0 && (errno == EOPNOTSUPP || errno == EINVAL))
+                    nowait_unsupported_.store(true, std::memory_order_relaxed);  // mincore from now on
+                break;
+            }
+            if (got == len) return true;
+            const int64_t o = off + got, n = len - got;  // the uncached rest
+            if (n >= (int64_t)kBlock && ((reinterpret_cast<uintptr_t>(dst + got) | (uint64_t)o) & (kBlock - 1)) == 0) {
+                const int64_t head = n & ~(int64_t)(kBlock - 1);
+                if (read_full(dfd_[f], dst + got, o, head)) {
+                    direct_bytes_.fetch_add((uint64_t)head, std::memory_order_relaxed);
+                    return head == n || read_full(buffered_fd, dst + got + head, o + head, n - head);
+                }
+            }
+            return read_full(buffered_fd, dst + got, o, n);
+        }
+        if (aligned && (mode_ == 2 || !resident(f, off))) {
             const int64_t head = len & ~(int64_t)(kBlock - 1);
             if (read_full(dfd_[f], dst, off, head)) {
                 direct_bytes_.fetch_add((uint64_t)head, std::memory_order_relaxed);
@@ -187,6 +219,7 @@ class DirectIo {
         return mincore(static_cast<uint8_t*>(map_[f]) + off, 1, &v) != 0 || (v & 1);  // unknown: stay buffered
     }
     const int mode_;
+    mutable std::atomic<bool> nowait_unsupported_{false};
     std::vector<int> dfd_;
     std::vector<void*> map_;
     std::vector<uint64_t> size_;
