@@ -67,6 +67,7 @@ def main():
             f.flush()
             os.fsync(f.fileno())
         exp = oracle.pool_digest_synth(0x5EED0005, 0, n, pl, last_index=n - 1, last_len=last, threads=threads)
+        cache_nodes = page_cache_nodes(path)
         pools = {}
         for name, env in configs:
             saved = {k: os.environ.get(k) for k in env}
@@ -115,7 +116,46 @@ def main():
     except Exception as e:  # noqa: BLE001  (diagnostic only)
         node = f"? ({e})"
     print(json.dumps({"config": "cpu_pool", "threads": threads, **cpu, "dir": d, "fs": bench.fs_type(d),
-                      "gpu_numa_node": node}))
+                      "gpu_numa_node": node, "page_cache_pages_by_node": cache_nodes}))
+
+
+def page_cache_nodes(path, samples=4096):
+    """NUMA node of a sample of the file's page-cache pages: map the file,
+    touch one byte per sampled page (a minor fault maps the cached page, no
+    copy) and ask move_pages(2) with nodes=NULL where each page lives."""
+    import ctypes
+    import mmap as _mmap
+
+    libc = ctypes.CDLL(None, use_errno=True)
+    size = os.path.getsize(path)
+    page = _mmap.PAGESIZE
+    with open(path, "rb") as f:
+        m = _mmap.mmap(f.fileno(), size, prot=_mmap.PROT_READ)
+        try:
+            import numpy as np
+
+            mv = memoryview(m)
+            a = np.frombuffer(mv, dtype=np.uint8)  # the mapping's address via the buffer protocol
+            start = a.ctypes.data
+            step = max(1, (size // page) // samples)
+            idx = list(range(0, size // page, step))
+            for i in idx:
+                _ = int(a[i * page])  # map the page
+            ptrs = (ctypes.c_void_p * len(idx))(*[start + i * page for i in idx])
+            status = (ctypes.c_int * len(idx))()
+            SYS_move_pages = 279  # x86_64
+            rc = libc.syscall(SYS_move_pages, 0, ctypes.c_ulong(len(idx)), ptrs, None, status, 0)
+            out = {}
+            if rc == 0:
+                for st in status:
+                    k = f"N{st}" if st >= 0 else f"err{-st}"
+                    out[k] = out.get(k, 0) + 1
+            else:
+                out["error"] = ctypes.get_errno()
+            del a, mv
+            return out
+        finally:
+            m.close()
 
 
 if __name__ == "__main__":
