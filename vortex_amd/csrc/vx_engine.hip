@@ -164,8 +164,9 @@ struct vx_ctx {
     // VX_VERIFY_DIRECT: 0 = never, 1 = when not cached (default), 2 = whenever aligned)
     int verify_direct = 1;
     // re-verify reader threads pinned to the CPUs of the GPU's NUMA node
-    // (gpu_numa_cpus; VX_VERIFY_NUMA=0 turns it off)
-    int verify_numa = 1;
+    // (gpu_numa_cpus; VX_VERIFY_NUMA=1).  Off by default: on the shared GPU
+    // hosts it was +5 % / -1 % / +2 % / -10 % across four boxes
+    int verify_numa = 0;
     uint64_t chunk_rounds = 0;  // chunk rounds launched (vx_tuning_chunk_rounds)
     // Per-piece device rows of the chunk paths (state | expected | digest |
     // verdict), kept across calls and grown on demand: allocating them per
