@@ -167,6 +167,9 @@ struct vx_ctx {
     // (gpu_numa_cpus; VX_VERIFY_NUMA=1).  Off by default: on the shared GPU
     // hosts it was +5 % / -1 % / +2 % / -10 % across four boxes
     int verify_numa = 0;
+    // re-verify: extra reader threads that read O_DIRECT even when the data is
+    // cached (vx_files::Readers helpers; VX_VERIFY_HELPERS=N)
+    int verify_helpers = 0;
     uint64_t chunk_rounds = 0;  // chunk rounds launched (vx_tuning_chunk_rounds)
     // Per-piece device rows of the chunk paths (state | expected | digest |
     // verdict), kept across calls and grown on demand: allocating them per
@@ -798,6 +801,7 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (const char* m = std::getenv("VX_VERIFY_READAHEAD")) c->verify_readahead = (uint32_t)std::max(1, std::atoi(m));
     if (const char* m = std::getenv("VX_VERIFY_DIRECT")) c->verify_direct = std::max(0, std::min(3, std::atoi(m)));
     if (const char* m = std::getenv("VX_VERIFY_NUMA")) c->verify_numa = std::atoi(m) != 0;
+    if (const char* m = std::getenv("VX_VERIFY_HELPERS")) c->verify_helpers = std::max(0, std::min(16, std::atoi(m)));
     int rc = set_device(c);
     if (!rc && c->h2d_mode == 3 && hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess)
         rc = fail(VX_EDEVICE, "vx_create: copy stream");
@@ -1899,7 +1903,8 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
         const vx_files::DirectIo dio(paths, fds, c->verify_direct);
         cpu_set_t numa;
         const bool pin = c->verify_numa && gpu_numa_cpus(c, &numa);
-        vx_files::Readers rd(nthreads, fs, fds, piece_length, bad.data(), first, &dio, pin ? &numa : nullptr);
+        vx_files::Readers rd(nthreads, fs, fds, piece_length, bad.data(), first, &dio, pin ? &numa : nullptr,
+                             c->verify_direct ? c->verify_helpers : 0);
         FileVerify fv{c, expected, matched_out, bad};
         c->harvest_counts_mismatches = false;
         rc = chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total, first, end, C)

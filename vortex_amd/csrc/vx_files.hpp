@@ -172,11 +172,12 @@ class DirectIo {
     DirectIo& operator=(const DirectIo&) = delete;
 
     // Read [off, off+len) of file f into dst; buffered_fd is the normal descriptor.
-    bool read(uint32_t f, int buffered_fd, uint8_t* dst, int64_t off, int64_t len) const {
+    // force: O_DIRECT whenever aligned, cached or not (the direct helpers).
+    bool read(uint32_t f, int buffered_fd, uint8_t* dst, int64_t off, int64_t len, bool force = false) const {
         const bool aligned = f < dfd_.size() && dfd_[f] >= 0 && len >= (int64_t)kBlock && off >= 0 &&
                              ((reinterpret_cast<uintptr_t>(dst) | (uint64_t)off) & (kBlock - 1)) == 0 &&
                              (uint64_t)(off + len) <= size_[f];
-        if (aligned && mode_ == 3 && !nowait_unsupported_.load(std::memory_order_relaxed)) {
+        if (aligned && mode_ == 3 && !force && !nowait_unsupported_.load(std::memory_order_relaxed)) {
             // Whatever the page cache holds comes back at once; the read stops
             // at the first page that would need the disk.
             int64_t got = 0;
@@ -202,7 +203,7 @@ class DirectIo {
             }
             return read_full(buffered_fd, dst + got, o, n);
         }
-        if (aligned && (mode_ == 2 || !resident(f, off))) {
+        if (aligned && (mode_ == 2 || force || !resident(f, off))) {
             const int64_t head = len & ~(int64_t)(kBlock - 1);
             if (read_full(dfd_[f], dst, off, head)) {
                 direct_bytes_.fetch_add((uint64_t)head, std::memory_order_relaxed);
@@ -228,14 +229,14 @@ class DirectIo {
 
 // Bytes [start, start+len) of a piece, mapped onto its file segments.
 inline bool read_range(const std::vector<FileSpan>& fs, const std::vector<int>& fds, uint32_t piece_length,
-                       const ReadItem& it, std::vector<Seg>& segs, const DirectIo* dio = nullptr) {
+                       const ReadItem& it, std::vector<Seg>& segs, const DirectIo* dio = nullptr, bool force = false) {
     segments(fs, (int64_t)it.piece, piece_length, segs);
     int64_t pos = 0, at = 0;
     const int64_t a = (int64_t)it.start, b = (int64_t)(it.start + it.len);
     for (const Seg& s : segs) {
         const int64_t lo = std::max<int64_t>(a, pos), hi = std::min<int64_t>(b, pos + s.len);
         if (lo < hi) {
-            const bool ok = dio ? dio->read(s.file, fds[s.file], it.dst + at, s.off + (lo - pos), hi - lo)
+            const bool ok = dio ? dio->read(s.file, fds[s.file], it.dst + at, s.off + (lo - pos), hi - lo, force)
                                 : read_full(fds[s.file], it.dst + at, s.off + (lo - pos), hi - lo);
             if (!ok) return false;
             at += hi - lo;
@@ -307,8 +308,14 @@ class Readers {
   public:
     // cpus (may be NULL): pin every reader thread to this set (the GPU's NUMA
     // node, vx_engine.hip gpu_numa_cpus); pinning is best effort.
+    // helpers: extra threads that read their items with O_DIRECT even when the
+    // data is cached (DirectIo force), so the drive's DMA adds to the CPU's
+    // page-cache copies on hosts where those copies are the limit; a helper
+    // whose direct read runs slower than kHelperMinRate stops for the call.
+    static constexpr double kHelperMinRate = 1.0e9;  // bytes per second
     Readers(int n, const std::vector<FileSpan>& fs, const std::vector<int>& fds, uint32_t piece_length,
-            uint8_t* bad, uint64_t first = 0, const DirectIo* dio = nullptr, const cpu_set_t* cpus = nullptr)
+            uint8_t* bad, uint64_t first = 0, const DirectIo* dio = nullptr, const cpu_set_t* cpus = nullptr,
+            int helpers = 0)
         : fs_(fs), fds_(fds), pl_(piece_length), bad_(bad), first_(first), dio_(dio) {
         if (cpus) {
             cpus_ = *cpus;
@@ -325,6 +332,13 @@ class Readers {
             }
         }
         if (th_.empty()) inline_ = true;  // not even one: submit() reads on the caller's thread
+        for (int t = 0; t < helpers && dio_ && !inline_; ++t) {
+            try {
+                th_.emplace_back([this] { loop(true); });
+            } catch (...) {
+                break;
+            }
+        }
     }
     ~Readers() {
         {
@@ -393,11 +407,12 @@ class Readers {
     // jobs), so the bad flag is stored atomically; the caller reads it after
     // wait(), which orders it through mu_.
     void mark_bad(uint64_t piece) { __atomic_store_n(&bad_[piece - first_], (uint8_t)1, __ATOMIC_RELAXED); }
-    void read_item(const ReadItem& it, std::vector<Seg>& segs) {
+    // Returns the item's read time in ns.
+    uint64_t read_item(const ReadItem& it, std::vector<Seg>& segs, bool force = false) {
         const uint64_t t0 = now_ns();
         uint64_t expect = 0;
         first_ns_.compare_exchange_strong(expect, t0, std::memory_order_relaxed);
-        read_item_impl(it, segs);
+        read_item_impl(it, segs, force);
         const uint64_t t1 = now_ns();
         busy_ns_.fetch_add(t1 - t0, std::memory_order_relaxed);
         bytes_.fetch_add(it.len, std::memory_order_relaxed);
@@ -406,15 +421,17 @@ class Readers {
         uint64_t last = last_ns_.load(std::memory_order_relaxed);
         while (last < t1 && !last_ns_.compare_exchange_weak(last, t1, std::memory_order_relaxed)) {
         }
+        return t1 - t0;
     }
-    void read_item_impl(const ReadItem& it, std::vector<Seg>& segs) {
+    void read_item_impl(const ReadItem& it, std::vector<Seg>& segs, bool force) {
         if (it.file >= 0) {
-            const bool ok = dio_ ? dio_->read((uint32_t)it.file, fds_[it.file], it.dst, it.file_off, (int64_t)it.len)
+            const bool ok = dio_ ? dio_->read((uint32_t)it.file, fds_[it.file], it.dst, it.file_off, (int64_t)it.len,
+                                              force)
                                  : read_full(fds_[it.file], it.dst, it.file_off, (int64_t)it.len);
             if (ok) return;
         }
         if (it.file < 0) {
-            if (!read_range(fs_, fds_, pl_, it, segs, dio_)) mark_bad(it.piece);
+            if (!read_range(fs_, fds_, pl_, it, segs, dio_, force)) mark_bad(it.piece);
             return;
         }
         for (uint32_t k = 0; k < it.pieces; ++k) {  // the run failed: piece by piece, as the walk reads
@@ -437,7 +454,7 @@ class Readers {
             if (jobs_[j].next < jobs_[j].items->size()) return (long)j;
         return -1;
     }
-    void loop() {
+    void loop(bool helper = false) {
         std::vector<Seg> segs;
         std::unique_lock<std::mutex> g(mu_);
         for (;;) {
@@ -447,9 +464,11 @@ class Readers {
             Job& j = jobs_[id - base_];
             const ReadItem& it = (*j.items)[j.next++];
             g.unlock();
-            read_item(it, segs);
+            const uint64_t ns = read_item(it, segs, helper);
             g.lock();
             if (--jobs_[id - base_].left == 0) retire();  // the job cannot have retired: left was > 0
+            if (helper && it.len >= (64u << 10) && (double)it.len * 1e9 < kHelperMinRate * (double)ns)
+                return;  // the drive is slower than the page cache could ever be: leave it to the readers
         }
     }
 
