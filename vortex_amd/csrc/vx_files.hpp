@@ -312,7 +312,7 @@ class Readers {
     // data is cached (DirectIo force), so the drive's DMA adds to the CPU's
     // page-cache copies on hosts where those copies are the limit; a helper
     // whose direct read runs slower than kHelperMinRate stops for the call.
-    static constexpr double kHelperMinRate = 1.0e9;  // bytes per second
+    static constexpr double kHelperMinRate = 0.2e9;  // bytes per second of one request (QD1)
     Readers(int n, const std::vector<FileSpan>& fs, const std::vector<int>& fds, uint32_t piece_length,
             uint8_t* bad, uint64_t first = 0, const DirectIo* dio = nullptr, const cpu_set_t* cpus = nullptr,
             int helpers = 0)
