@@ -771,11 +771,27 @@ def main() -> int:
         dist.barrier()
     elapsed = t1 - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    ranks = None
     if distributed:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64,
-                         device=dev if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+        # The verdict all-gather alone, after the timed region: what the one
+        # collective costs per step (the scaling overhead at N > 1).
+        # (wall clock: RCCL runs on its own stream, gloo on the host)
+        torch.cuda.synchronize()
+        g0 = time.perf_counter()
+        for _ in range(args.steps):
+            gather_verdicts(matched, n_total)
+        torch.cuda.synchronize()
+        gather_ms = (time.perf_counter() - g0) / args.steps * 1e3
+        # every rank's figures (max over ranks is what `value` uses)
+        mine = torch.tensor([elapsed, kern_ms, gather_ms], dtype=torch.float64,
+                            device=dev if args.dist_backend == "nccl" else "cpu")
+        allr = torch.empty(3 * world, dtype=torch.float64, device=mine.device)
+        dist.all_gather_into_tensor(allr, mine)
+        per = allr.view(world, 3).cpu().tolist()
+        elapsed, kern_ms = max(r[0] for r in per), max(r[1] for r in per)
+        ranks = {"step_ms": [round(r[0] / args.steps * 1e3, 4) for r in per],
+                 "kernel_ms": [round(r[1], 4) for r in per],
+                 "verdict_gather_ms": [round(r[2], 4) for r in per]}
 
     # Verdicts: exactly the corrupted pieces mismatch (checked on the gathered
     # table when N > 1, else locally).
@@ -810,6 +826,8 @@ def main() -> int:
                    "parallelism": f"piece-index shard x{world}"},
         "roofline": roofline(n, plen, kern_ms, achieved, workload),
     }
+    if ranks is not None:
+        res["ranks"] = ranks
     if rank == 0 and world == 1:
         # Extra legs (N=1 only): the other BASELINE configs and
         # the host-resident path, each with its own correctness check.  A leg

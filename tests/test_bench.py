@@ -80,6 +80,9 @@ def test_plain_bench_launches_its_ranks(built, gpu, n):
     assert res["n_gpus"] == n and res["world_size"] == n and res["backend"] == "gloo"
     assert res["value"] > 0 and res["config"]["pieces_per_gpu"] == 1024
     assert res["config"]["total_GiB"] == n * 1024 * 256 / (1 << 20)
+    rk = res["ranks"]  # every rank's step, kernel and verdict-gather times
+    assert all(len(rk[k]) == n for k in ("step_ms", "kernel_ms", "verdict_gather_ms"))
+    assert max(rk["step_ms"]) == pytest.approx(res["ms_per_step"], rel=1e-3)
 
 
 @pytest.mark.gpu
@@ -95,3 +98,4 @@ def test_bench_rccl_world_size_1(built, gpu):
     (res,) = _lines(r.stdout)
     assert res["n_gpus"] == 1 and res["world_size"] == 1 and res["backend"] == "nccl"
     assert "nccl all-gather of verdicts" in res["config"]["workload"]
+    assert len(res["ranks"]["verdict_gather_ms"]) == 1 and res["ranks"]["verdict_gather_ms"][0] > 0
