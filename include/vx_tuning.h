@@ -28,6 +28,10 @@ uint64_t vx_tuning_chunk_rounds(const struct vx_ctx* ctx);
 /* 64 KiB tiles the context's gather kernel has pulled from registered host
  * buffers (async / batch slots). */
 uint64_t vx_tuning_gather_tiles(const struct vx_ctx* ctx);
+/* Slots the context hashed with the zero-copy kernel (VX_ZERO_COPY=1: every
+ * piece registered and aligned, read from host memory by the hash kernel
+ * itself, no gather). */
+uint64_t vx_tuning_zero_copy_slots(const struct vx_ctx* ctx);
 /* Fault injection for tests: after k more successful piece submits (async or
  * inside a host batch), the next one fails with VX_ENOMEM without latching
  * the context, as a failed pinned-stage allocation does.  k < 0 turns it off. */

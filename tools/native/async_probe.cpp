@@ -10,7 +10,7 @@
 // (event_loop.rs:554-557).  Every completion must match.  Prints one JSON
 // line: GiB/s of piece bytes submitted → verdict polled.
 //
-// usage: async_probe <piece_len> [nbuf=1024] [total_GiB=8] [flush_every=64] [registered=1] [slot_MiB=default]
+// usage: async_probe <piece_len> [nbuf=1024] [total_GiB=8] [flush_every=64] [registered=1] [slot_MiB=default (0)] [slots=4]
 //   registered: 0 = plain memory (staged), 1 = one registered mmap holding all
 //   buffers, 2 = one mmap per buffer, each registered (vortex's BufferPool,
 //   buf_pool.rs:92-98)
@@ -46,10 +46,11 @@ int main(int argc, char** argv) {
 
     vx_config cfg;
     vx_config_default(&cfg, plen);
-    if (argc > 6) {
+    if (argc > 6 && std::strtoull(argv[6], nullptr, 0) > 0) {
         cfg.slot_bytes = std::strtoull(argv[6], nullptr, 0) << 20;
         cfg.batch_pieces = (uint32_t)std::min<uint64_t>(65536, cfg.slot_bytes / ((plen + 255) / 256 * 256));
     }
+    if (argc > 7) cfg.slots = (uint32_t)std::atoi(argv[7]);  // batch slots (default 4)
     vx_ctx* ctx = nullptr;
     if (int rc = vx_create(&cfg, &ctx)) {
         std::fprintf(stderr, "vx_create: %d %s\n", rc, vx_last_error());

@@ -795,6 +795,176 @@ hipError_t launch_chunk(const uint8_t* base, const uint64_t* offsets, const uint
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Zero-copy split kernel: the async path's slots of
+// registered pieces are hashed straight out of host memory through the
+// pieces' device mappings (srcs[i], 16-byte aligned), with no gather kernel,
+// so a slot's PCIe transfer overlaps its own hashing instead of preceding it.
+// Same pair and ring protocol as sha1_ragged_split_kernel; the producer's
+// loads differ.  Over PCIe the load SHAPE decides the rate
+// (tools/native/zc_pattern_probe.hip): one lane per piece, as the HBM kernels
+// load, reaches 28-31 GiB/s; 16 lanes per piece, 256 contiguous bytes of each
+// of 4 pieces per wave instruction, 51-53 GiB/s once ~1 MiB is in flight.
+//
+// A pair hashes kZcPieces = 32 pieces (lanes 32-63 mirror lanes 0-31 and
+// emit nothing): the chain per block is the same at 32 or 64 live lanes, the
+// async slots leave most CUs idle, and so every piece gets twice the bytes in
+// flight — a tile is 8 blocks (512 B) of all 32 pieces, 16 wave instructions,
+// and two tiles (32 KiB) are in flight per producer wave, 1 KiB per piece.
+// A landed tile is transposed through a 16 KiB LDS stage (chunk c of piece p
+// at [c][(p + c) & 31]: conflict-free both ways) to the lane that owns the
+// piece.  Chunks past a piece's full blocks load the device zero line, so no
+// load reaches past a piece; the < 64-byte tail and the padding come from the
+// lane's own bytes (tail_words), as in the ragged kernel's phase 2.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kZcPieces = 32;      // pieces per pair
+constexpr uint32_t kZcTileBlocks = 8;   // 64-byte blocks per piece per tile
+constexpr uint32_t kZcChunks = kZcTileBlocks * 4;  // 16-byte chunks per piece per tile
+
+typedef uint32_t U32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) U32x4 GlobalU32x4;
+
+// Tile t's 16 loads: instruction k reads 16 bytes at ztab[k][lane].xy +
+// t*512 (this lane's chunk of its piece) when that chunk lies inside the
+// piece's full blocks (t*512 + chunk_end <= ztab[k][lane].z), else the zero
+// line.  Explicitly global loads: the pointers come from memory, and as flat
+// loads they would also count in lgkmcnt, which every ring barrier drains.
+__device__ __forceinline__ void zc_load_tile(uint4 (&r)[16], const uint4 (*ztab)[64], int lane, uint32_t chunk_end,
+                                             uint64_t t) {
+    const uint64_t o = t * (kZcTileBlocks * 64);
+    const uint64_t zero = reinterpret_cast<uint64_t>(g_zero_line);
+    uint64_t addr[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint4 e = ztab[k][lane];
+        const uint64_t base = ((uint64_t)e.y << 32) | e.x;
+        addr[k] = o + (k >= 8 ? chunk_end + 256 : chunk_end) <= e.z ? base + o : zero;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {  // a native vector load: a uint4 struct copy from AS1 became a memcpy
+        const U32x4 v = *reinterpret_cast<GlobalU32x4*>(addr[k]);  // that kept the tiles in scratch
+        r[k] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int S>
+__global__ __launch_bounds__(kPairBlock) void sha1_zc_split_kernel(const uint64_t* __restrict__ srcs,
+                                                                   const uint32_t* __restrict__ lens, uint32_t n,
+                                                                   uint8_t* __restrict__ digests,
+                                                                   const uint8_t* __restrict__ expected,
+                                                                   uint8_t* __restrict__ matched,
+                                                                   const uint32_t* __restrict__ exp_index) {
+    __shared__ RingLds<S> lds;
+    __shared__ uint4 stage[kZcChunks][kZcPieces];
+    __shared__ uint4 ztab[16][64];  // per load instruction and lane: {source lo, hi, full-block bytes, 0}
+    const int lane = threadIdx.x & 63;
+    const uint32_t pl = lane & (kZcPieces - 1);  // the piece this lane hashes (lanes 32-63 mirror 0-31)
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t g0 = blockIdx.x * kZcPieces;
+    const uint32_t j = g0 + pl;
+    const uint32_t jj = j < n ? j : n - 1;
+    const uint32_t len = lens[jj];
+    const uint32_t nfull = len >> 6;
+    const uint32_t rem = len & 63u;
+    const uint32_t nb = nfull + (rem <= 55 ? 1u : 2u);
+    const uint32_t nb_wave = __builtin_amdgcn_readfirstlane(wave_max(nb));
+
+    if (wave == 1) {
+        // ---------------- producer ----------------
+        // Load instruction k covers pieces 4(k & 7) .. +3 (16 lanes each) and
+        // the (k >> 3)-th 256-byte half of the tile: this lane moves chunk
+        // c16 + 16(k >> 3) of piece 4(k & 7) + (lane >> 4).  The 16
+        // (source, limit) pairs live in LDS, not in 48 VGPRs.
+        const uint32_t c16 = lane & 15;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t pk = g0 + 4 * k + (lane >> 4);
+            const uint32_t pkk = pk < n ? pk : n - 1;
+            const uint32_t full = pk < n ? (lens[pkk] >> 6) * 64u : 0u;
+            const uint64_t base = srcs[pkk] + 16 * c16;
+            ztab[k][lane] = make_uint4((uint32_t)base, (uint32_t)(base >> 32), full, 0u);
+            ztab[k + 8][lane] = make_uint4((uint32_t)(base + 256), (uint32_t)((base + 256) >> 32), full, 0u);
+        }
+        const uint32_t chunk_end = 16 * c16 + 16;  // (+256 for the second half, zc_load_tile)
+        // this lane's padding block 0 (its own tail bytes, read once)
+        uint32_t padw[16];
+        const uint8_t* q = reinterpret_cast<const uint8_t*>(srcs[jj]) + (size_t)nfull * 64;
+        tail_words(padw, q, rem);
+        const uint32_t bits_hi = (uint32_t)(((uint64_t)len * 8u) >> 32);
+        const uint32_t bits_lo = (uint32_t)((uint64_t)len * 8u);
+        if (rem <= 55) {
+            padw[14] = bits_hi;
+            padw[15] = bits_lo;
+        }
+        // Two register tiles in flight, as two plain arrays and the tile body
+        // written out for each (as a loop over a ring[2][16], or through a
+        // lambda taking the tile by reference, hipcc kept the tiles in scratch).
+        uint4 ra[16], rb[16];
+        zc_load_tile(ra, ztab, lane, chunk_end, 0);
+        zc_load_tile(rb, ztab, lane, chunk_end, 1);
+        uint32_t w[16];
+        // Stage the landed tile REG, refill REG with tile T + 2, then hash
+        // tile T's (up to) 8 blocks.
+#define VX_ZC_TILE(REG, T)                                                                              \
+    {                                                                                                   \
+        const uint32_t t = (T);                                                                         \
+        _Pragma("unroll") for (int k = 0; k < 16; ++k) {                                                \
+            const uint32_t p = 4 * (k & 7) + (lane >> 4), c = c16 + 16 * (k >> 3);                      \
+            stage[c][(p + c) & (kZcPieces - 1)] = REG[k];                                               \
+        }                                                                                               \
+        zc_load_tile(REG, ztab, lane, chunk_end, t + 2);                                                \
+        _Pragma("unroll") for (uint32_t bb = 0; bb < kZcTileBlocks; ++bb) {                             \
+            const uint32_t b = kZcTileBlocks * t + bb;                                                  \
+            if (b < nb_wave) { /* wave-uniform */                                                       \
+                const uint4 q0 = stage[4 * bb + 0][(pl + 4 * bb + 0) & (kZcPieces - 1)];                 \
+                const uint4 q1 = stage[4 * bb + 1][(pl + 4 * bb + 1) & (kZcPieces - 1)];                 \
+                const uint4 q2 = stage[4 * bb + 2][(pl + 4 * bb + 2) & (kZcPieces - 1)];                 \
+                const uint4 q3 = stage[4 * bb + 3][(pl + 4 * bb + 3) & (kZcPieces - 1)];                 \
+                le_words(w, q0, q1, q2, q3);                                                            \
+                const bool is_pad0 = b == nfull;                                                        \
+                const bool is_pad1 = b == nfull + 1;                                                    \
+                _Pragma("unroll") for (int k = 0; k < 16; ++k) {                                        \
+                    uint32_t v = b < nfull ? w[k] : 0u;                                                 \
+                    v = is_pad0 ? padw[k] : v;                                                          \
+                    if (k >= 14) v = (is_pad1 && rem > 55) ? (k == 14 ? bits_hi : bits_lo) : v;         \
+                    w[k] = v;                                                                           \
+                }                                                                                       \
+                expand_store(w, lds.w[ring_slot<S>(b)], lane);                                          \
+                publish<S>(b); /* lgkmcnt(0) + s_barrier: stage reads done before it is rewritten */   \
+            }                                                                                           \
+        }                                                                                               \
+    }
+        // Straight-line trips (tiles past the data load the zero line, blocks
+        // past nb_wave are skipped), so the waitcnt pass sees the same 32
+        // loads in flight at the back edge as at the entry and waits for
+        // exactly the 16 of the tile it stages next.
+        const uint32_t ntiles = (nb_wave + kZcTileBlocks - 1) / kZcTileBlocks;
+        for (uint32_t t0 = 0; t0 < ntiles; t0 += 2) {
+            VX_ZC_TILE(ra, t0)
+            VX_ZC_TILE(rb, t0 + 1)
+        }
+#undef VX_ZC_TILE
+        producer_done<S>(nb_wave);
+    } else {
+        // ---------------- consumer ----------------
+        const uint32_t b1 = __builtin_amdgcn_readfirstlane(wave_min(nb));
+        State s = iv();
+        consume<S, true>(s, lds, lane, nb_wave, b1, nb);
+        if (lane < (int)kZcPieces && j < n) emit(s, j, digests, expected, matched, exp_index);
+    }
+}
+
+hipError_t launch_zero_copy(const uint64_t* srcs, const uint32_t* lens, uint32_t n, uint8_t* digests,
+                            const uint8_t* expected, uint8_t* matched, hipStream_t stream, const uint32_t* exp_index) {
+    if (n == 0) return hipSuccess;
+    const uint32_t blocks = (n + kZcPieces - 1) / kZcPieces;
+    hipLaunchKernelGGL(sha1_zc_split_kernel<kSplitSlots>, dim3(blocks), dim3(kPairBlock), 0, stream, srcs, lens, n,
+                       digests, expected, matched, exp_index);
+    return hipGetLastError();
+}
+
 template <int R, bool kAlias = false, bool kFence = false>
 hipError_t launch_uniform_lane_r(const uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint8_t* digests,
                                  const uint8_t* expected, uint8_t* matched, hipStream_t stream,

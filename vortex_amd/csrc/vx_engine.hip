@@ -129,6 +129,7 @@ struct Slot {
     bool uniform = true;
     bool has_expected = false;
     bool use_table = false;  // expected digests come from the device piece table
+    bool all_mapped = true;  // every non-empty piece is registered and 16-byte aligned (zero-copy candidate)
     enum State { FREE, FILLING, INFLIGHT } state = FREE;
     uint64_t seq = 0;
     std::chrono::steady_clock::time_point t_open{};  // first piece queued (vx_stats batch latency)
@@ -200,6 +201,11 @@ struct vx_ctx {
     // separately registered buffers: 29.7 -> 35.7 GiB/s.
     std::unordered_map<uintptr_t, Reg> registered_at;
     bool gather = true;        // VX_GATHER=0 turns the gather kernel off (A/B)
+    // VX_ZERO_COPY=1: a slot whose pieces are all registered and aligned is
+    // hashed straight out of host memory by the zero-copy kernel, without a
+    // gather (sha1_zc_split_kernel; A/B)
+    bool zero_copy = false;
+    uint64_t zero_copy_slots = 0;  // slots hashed that way (vx_tuning_zero_copy_slots)
     uint32_t gather_grid = 0;  // VX_GATHER_GRID: workgroups per gather launch (0 = default)
     uint64_t gather_tiles = 0;  // tiles gathered (vx_tuning_gather_tiles)
     uint64_t pending = 0;
@@ -336,6 +342,7 @@ void reset_fill(Slot& s) {
     s.uniform = true;
     s.has_expected = false;
     s.use_table = false;
+    s.all_mapped = true;
 }
 
 int launch_slot_impl(vx_ctx* c, int si);
@@ -486,18 +493,25 @@ int launch_slot_impl(vx_ctx* c, int si) {
         return 0;
     }
     hipStream_t cs = c->h2d_mode == 3 ? c->copy_stream : s.stream;
+    // Zero-copy slot: every piece is read by the hash kernel itself, so no
+    // bytes cross PCIe ahead of it and nothing waits for the copy chain.
+    const bool zc = c->zero_copy && s.gtiles && s.all_mapped;
     stage_copies(s);
-    if (int rc = chain_h2d(c, si)) return rc;
+    if (!zc)
+        if (int rc = chain_h2d(c, si)) return rc;
     for (const DirectRun& r : s.druns)
         VX_HIP(hipMemcpyAsync(s.d_arena + r.lo, r.host, r.hi - r.lo, hipMemcpyHostToDevice, cs));
     for (const Run& r : s.runs)
         VX_HIP(hipMemcpyAsync(s.d_arena + r.lo, s.h_stage + r.lo, r.hi - r.lo, hipMemcpyHostToDevice, cs));
     const uint32_t n = s.n;
-    if (!s.uniform || s.gtiles) {
+    if (!zc && (!s.uniform || s.gtiles)) {
         VX_HIP(hipMemcpyAsync(s.d_offsets, s.h_offsets, (size_t)n * 8, hipMemcpyHostToDevice, cs));
         VX_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)n * 4, hipMemcpyHostToDevice, cs));
     }
-    if (s.gtiles) {
+    if (zc) {
+        VX_HIP(hipMemcpyAsync(s.d_lens, s.h_lens, (size_t)n * 4, hipMemcpyHostToDevice, cs));
+        VX_HIP(hipMemcpyAsync(s.d_src, s.h_src, (size_t)n * 8, hipMemcpyHostToDevice, cs));
+    } else if (s.gtiles) {
         VX_HIP(hipMemcpyAsync(s.d_src, s.h_src, (size_t)n * 8, hipMemcpyHostToDevice, cs));
         VX_HIP(hipMemcpyAsync(s.d_tfirst, s.h_tfirst, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, cs));
         // Slots of long pieces (>= 2 MiB on average) hash with a few
@@ -521,7 +535,10 @@ int launch_slot_impl(vx_ctx* c, int si) {
     if (cs != s.stream) VX_HIP(hipStreamWaitEvent(s.stream, s.copied, 0));
     mark_launched(c, si);
     hipError_t e;
-    if (s.uniform) {
+    if (zc) {
+        e = vx::launch_zero_copy(s.d_src, s.d_lens, n, s.d_digests, d_exp, s.d_matched, s.stream, d_row);
+        c->zero_copy_slots++;
+    } else if (s.uniform) {
         const uint32_t len = s.h_lens[0];
         const uint64_t stride = align_up(std::max<uint32_t>(len, 1), kAlign);
         e = vx::launch_uniform(s.d_arena, stride, len, n, s.d_digests, d_exp, s.d_matched, s.stream,
@@ -662,6 +679,7 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
         s->h_src[i] = reinterpret_cast<uint64_t>(dev);
         s->gtiles += vx::gather_tiles(len);
     } else if (len) {
+        s->all_mapped = false;
         if (is_registered(c, data, len)) {
             // Pinned source: DMA straight from the caller's buffer at launch;
             // pieces adjacent in host memory AND in the arena share one copy.
@@ -788,6 +806,7 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (const char* m = std::getenv("VX_H2D_MODE")) c->h2d_mode = std::atoi(m) & 3;
     if (const char* m = std::getenv("VX_GATHER")) c->gather = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_GATHER_GRID")) c->gather_grid = (uint32_t)std::atoi(m);
+    if (const char* m = std::getenv("VX_ZERO_COPY")) c->zero_copy = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_LAZY_FLUSH")) c->lazy_flush = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_BATCH_SORT")) c->batch_sort = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_BATCH_CHUNK")) c->batch_chunk = align_up(std::strtoull(m, nullptr, 0), kAlign);
@@ -2118,6 +2137,8 @@ int vx_reset_stats(vx_ctx* c) {
 
 uint64_t vx_tuning_chunk_rounds(const vx_ctx* c) { return c ? c->chunk_rounds : 0; }
 uint64_t vx_tuning_gather_tiles(const vx_ctx* c) { return c ? c->gather_tiles : 0; }
+
+uint64_t vx_tuning_zero_copy_slots(const vx_ctx* c) { return c ? c->zero_copy_slots : 0; }
 int vx_tuning_last_verify(const vx_ctx* c, vx_verify_trace* out) {
     if (!c || !out) return fail(VX_EINVAL, "vx_tuning_last_verify: NULL argument");
     *out = c->last_verify;

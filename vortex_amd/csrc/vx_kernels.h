@@ -73,6 +73,14 @@ uint32_t gather_tiles(uint32_t len);
 hipError_t launch_gather(const uint64_t* src, const uint64_t* dst_off, const uint32_t* lens, const uint32_t* tfirst,
                          uint32_t n, uint32_t ntiles, uint8_t* arena, hipStream_t stream, uint32_t max_grid = 0);
 
+// Zero-copy split kernel: piece i is read straight from
+// registered host memory at its device-mapped address srcs[i] (16-byte
+// aligned, lens[i] bytes; srcs[i] may be 0 when lens[i] == 0); digests /
+// matched row i (expected row exp_index[i] when given).
+hipError_t launch_zero_copy(const uint64_t* srcs, const uint32_t* lens, uint32_t n, uint8_t* digests,
+                            const uint8_t* expected, uint8_t* matched, hipStream_t stream,
+                            const uint32_t* exp_index = nullptr);
+
 hipError_t launch_synth_fill(uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint64_t first,
                              uint64_t seed, uint32_t corrupt_every, hipStream_t stream);
 
