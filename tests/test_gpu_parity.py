@@ -758,6 +758,7 @@ def test_scattered_registered_pieces(built, gpu, monkeypatch, gather):
     from vortex_amd.hash_pool import HashPool
 
     monkeypatch.setenv("VX_GATHER", gather)
+    monkeypatch.setenv("VX_ZERO_COPY", "0")  # the gather path itself (zero-copy slots: test_gpu_zero_copy.py)
     rng = random.Random(5)
     lens = [0, 1, 15, 16, 17, 63, 64, 65, 4095, 65535, 65536, 65537, 131072 + 48, 200000, (1 << 20) + 3, 300]
     lens = lens * 6

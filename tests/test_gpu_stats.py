@@ -27,8 +27,10 @@ def _check_latency(st):
         assert st["batch_latency_max_us"] >> top in (1, 0) or top == len(st["batch_latency_hist"]) - 1
 
 
-def test_stats_async_path(built, gpu):
+def test_stats_async_path(built, gpu, monkeypatch):
     from vortex_amd.hash_pool import HashPool
+
+    monkeypatch.setenv("VX_ZERO_COPY", "0")  # counts the gather kernel's tiles (zero-copy: test_gpu_zero_copy.py)
 
     rng = random.Random(8)
     plen = 16384 * 3 + 96  # 16-byte multiple: registered pieces go through the gather kernel

@@ -2,7 +2,8 @@
 # tools/native/async_probe with VX_ZERO_COPY=0 (gather kernel + hash) and =1
 # (the hash kernel reads the registered pieces itself), alternating per rep,
 # one registered mmap per pool buffer (vortex's BufferPool), flush every 64.
-#   /usr/local/graft/bin/gpurun --timeout 900 -- bash tools/ab_zero_copy.sh [tag] [reps]
+# ZC_VALUES="0 2" compares the gather against the default policy instead.
+#   /usr/local/graft/bin/gpurun --timeout 900 -- bash tools/ab_zero_copy.sh [tag] [reps] ["piece_len:nbuf:GiB ..."]
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out/r03/zc
@@ -10,11 +11,11 @@ OUT=gpurun_out/r03/zc/ab_${1:-run}.jsonl
 : > $OUT
 REPS=${2:-3}
 # piece_len nbuf total_GiB
-CASES="262144:8192:2 262144:8192:8 16384:8192:1 1048576:2048:4 2097152:1024:4 4194304:512:4"
+CASES=${3:-"262144:8192:2 262144:8192:8 16384:8192:1 1048576:2048:4 2097152:1024:4 4194304:512:4"}
 for rep in $(seq 1 $REPS); do
   for c in $CASES; do
     IFS=: read pl nbuf gib <<< "$c"
-    for zc in 0 1; do
+    for zc in ${ZC_VALUES:-0 1}; do
       line=$(VX_ZERO_COPY=$zc timeout -k 10 120 ./tools/native/async_probe $pl $nbuf $gib 64 2) || { echo "FAIL pl=$pl zc=$zc"; exit 1; }
       echo "{\"zc\": $zc, \"rep\": $rep, \"piece_len\": $pl, \"GiB\": $gib, \"res\": $line}" >> $OUT
     done

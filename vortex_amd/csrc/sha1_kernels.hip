@@ -859,6 +859,7 @@ __global__ __launch_bounds__(kPairBlock) void sha1_zc_split_kernel(const uint64_
     __shared__ RingLds<S> lds;
     __shared__ uint4 stage[kZcChunks][kZcPieces];
     __shared__ uint4 ztab[16][64];  // per load instruction and lane: {source lo, hi, full-block bytes, 0}
+    __shared__ uint4 padl[4][64];   // each lane's padding block 0 (kept out of VGPRs)
     const int lane = threadIdx.x & 63;
     const uint32_t pl = lane & (kZcPieces - 1);  // the piece this lane hashes (lanes 32-63 mirror 0-31)
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -898,9 +899,16 @@ __global__ __launch_bounds__(kPairBlock) void sha1_zc_split_kernel(const uint64_
             padw[14] = bits_hi;
             padw[15] = bits_lo;
         }
-        // Two register tiles in flight, as two plain arrays and the tile body
-        // written out for each (as a loop over a ring[2][16], or through a
-        // lambda taking the tile by reference, hipcc kept the tiles in scratch).
+#pragma unroll
+        for (int k = 0; k < 4; ++k) padl[k][lane] = make_uint4(padw[4 * k], padw[4 * k + 1], padw[4 * k + 2], padw[4 * k + 3]);
+        // The wave's first block that is not data for every lane: blocks
+        // before it need no select (and no padding words).
+        const uint32_t b_sel = __builtin_amdgcn_readfirstlane(wave_min(nfull));
+        // Two register tiles in flight (32 KiB per wave; a third measured no
+        // faster, profiles/r03/zero_copy/ab_async_t3.jsonl), as plain arrays
+        // with the tile body written out for each (as a loop over a
+        // ring[2][16], or through a lambda taking the tile by reference,
+        // hipcc kept the tiles in scratch).
         uint4 ra[16], rb[16];
         zc_load_tile(ra, ztab, lane, chunk_end, 0);
         zc_load_tile(rb, ztab, lane, chunk_end, 1);
@@ -923,13 +931,18 @@ __global__ __launch_bounds__(kPairBlock) void sha1_zc_split_kernel(const uint64_
                 const uint4 q2 = stage[4 * bb + 2][(pl + 4 * bb + 2) & (kZcPieces - 1)];                 \
                 const uint4 q3 = stage[4 * bb + 3][(pl + 4 * bb + 3) & (kZcPieces - 1)];                 \
                 le_words(w, q0, q1, q2, q3);                                                            \
-                const bool is_pad0 = b == nfull;                                                        \
-                const bool is_pad1 = b == nfull + 1;                                                    \
-                _Pragma("unroll") for (int k = 0; k < 16; ++k) {                                        \
-                    uint32_t v = b < nfull ? w[k] : 0u;                                                 \
-                    v = is_pad0 ? padw[k] : v;                                                          \
-                    if (k >= 14) v = (is_pad1 && rem > 55) ? (k == 14 ? bits_hi : bits_lo) : v;         \
-                    w[k] = v;                                                                           \
+                if (b >= b_sel) { /* wave-uniform: some lane is past its data */                        \
+                    const uint4 p0 = padl[0][lane], p1 = padl[1][lane], p2 = padl[2][lane], p3 = padl[3][lane]; \
+                    const uint32_t pw[16] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w,            \
+                                             p2.x, p2.y, p2.z, p2.w, p3.x, p3.y, p3.z, p3.w};           \
+                    const bool is_pad0 = b == nfull;                                                    \
+                    const bool is_pad1 = b == nfull + 1;                                                \
+                    _Pragma("unroll") for (int k = 0; k < 16; ++k) {                                    \
+                        uint32_t v = b < nfull ? w[k] : 0u;                                             \
+                        v = is_pad0 ? pw[k] : v;                                                        \
+                        if (k >= 14) v = (is_pad1 && rem > 55) ? (k == 14 ? bits_hi : bits_lo) : v;     \
+                        w[k] = v;                                                                       \
+                    }                                                                                   \
                 }                                                                                       \
                 expand_store(w, lds.w[ring_slot<S>(b)], lane);                                          \
                 publish<S>(b); /* lgkmcnt(0) + s_barrier: stage reads done before it is rewritten */   \

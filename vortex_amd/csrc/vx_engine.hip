@@ -69,6 +69,10 @@ int hip_fail(hipError_t e, const char* what) {
     } while (0)
 
 constexpr uint64_t kAlign = 256;
+// zc_wins: the mean piece lengths where gather + hash beats the zero-copy
+// kernel, and the slot size below which a batch is latency-bound
+constexpr uint64_t kZcBelow = 128 * 1024, kZcFrom = 512 * 1024;
+constexpr uint32_t kZcMinPieces = 128;
 
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
@@ -201,10 +205,11 @@ struct vx_ctx {
     // separately registered buffers: 29.7 -> 35.7 GiB/s.
     std::unordered_map<uintptr_t, Reg> registered_at;
     bool gather = true;        // VX_GATHER=0 turns the gather kernel off (A/B)
-    // VX_ZERO_COPY=1: a slot whose pieces are all registered and aligned is
-    // hashed straight out of host memory by the zero-copy kernel, without a
-    // gather (sha1_zc_split_kernel; A/B)
-    bool zero_copy = false;
+    // A slot whose pieces are all registered and aligned may be hashed
+    // straight out of host memory by the zero-copy kernel, without a gather
+    // (sha1_zc_split_kernel).  VX_ZERO_COPY: 0 = never,
+    // 1 = always, 2 = by the slot's mean piece length (zc_wins, default).
+    int zero_copy = 2;
     uint64_t zero_copy_slots = 0;  // slots hashed that way (vx_tuning_zero_copy_slots)
     uint32_t gather_grid = 0;  // VX_GATHER_GRID: workgroups per gather launch (0 = default)
     uint64_t gather_tiles = 0;  // tiles gathered (vx_tuning_gather_tiles)
@@ -482,6 +487,23 @@ int launch_slot(vx_ctx* c, int si) {
     return rc;
 }
 
+// Where the zero-copy kernel beats gather + hash (profiles/r03/zero_copy/):
+// on full async slots, by the slot's mean piece length (tools/ab_zero_copy.sh,
+// alternating runs of async_probe, one registered mmap per buffer): 16 KiB
+// 33 -> 45-48 GiB/s, 1 / 2 / 4 MiB 44 -> 48 / 34 -> 41-44 / 30 -> 35, equal
+// at 64-512 KiB but 1-6 % behind around 256 KiB on a long stream.  A small
+// batch is latency-bound instead: its gather is short and its chain then runs
+// from HBM, 6-8 % faster per block than reading host memory as it goes
+// (tools/loop_latency_ab.py: download-loop p50 at 2 / 4 MiB 27.3 / 67.4 ms
+// against 28.8-29.5 / 71.6), so it keeps the gather.
+bool zc_wins(const Slot& s) {
+    if (s.n < kZcMinPieces) return false;
+    uint64_t bytes = 0;
+    for (uint32_t i = 0; i < s.n; ++i) bytes += s.h_lens[i];
+    const uint64_t mean = bytes / std::max<uint32_t>(s.n, 1);
+    return mean < kZcBelow || mean >= kZcFrom;
+}
+
 int launch_slot_impl(vx_ctx* c, int si) {
     Slot& s = c->slots[si];
     if (c->filling == si) {
@@ -495,7 +517,7 @@ int launch_slot_impl(vx_ctx* c, int si) {
     hipStream_t cs = c->h2d_mode == 3 ? c->copy_stream : s.stream;
     // Zero-copy slot: every piece is read by the hash kernel itself, so no
     // bytes cross PCIe ahead of it and nothing waits for the copy chain.
-    const bool zc = c->zero_copy && s.gtiles && s.all_mapped;
+    const bool zc = s.gtiles && s.all_mapped && (c->zero_copy == 1 || (c->zero_copy == 2 && zc_wins(s)));
     stage_copies(s);
     if (!zc)
         if (int rc = chain_h2d(c, si)) return rc;
@@ -806,7 +828,7 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (const char* m = std::getenv("VX_H2D_MODE")) c->h2d_mode = std::atoi(m) & 3;
     if (const char* m = std::getenv("VX_GATHER")) c->gather = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_GATHER_GRID")) c->gather_grid = (uint32_t)std::atoi(m);
-    if (const char* m = std::getenv("VX_ZERO_COPY")) c->zero_copy = std::atoi(m) != 0;
+    if (const char* m = std::getenv("VX_ZERO_COPY")) c->zero_copy = std::max(0, std::min(2, std::atoi(m)));
     if (const char* m = std::getenv("VX_LAZY_FLUSH")) c->lazy_flush = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_BATCH_SORT")) c->batch_sort = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_BATCH_CHUNK")) c->batch_chunk = align_up(std::strtoull(m, nullptr, 0), kAlign);
