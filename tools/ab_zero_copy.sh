@@ -2,7 +2,8 @@
 # tools/native/async_probe with VX_ZERO_COPY=0 (gather kernel + hash) and =1
 # (the hash kernel reads the registered pieces itself), alternating per rep,
 # one registered mmap per pool buffer (vortex's BufferPool), flush every 64.
-# ZC_VALUES="0 2" compares the gather against the default policy instead.
+# ZC_VALUES="0 2" compares the gather against the default policy instead;
+# REG=1 puts every buffer in one registered mmap (async_probe registered=1).
 #   /usr/local/graft/bin/gpurun --timeout 900 -- bash tools/ab_zero_copy.sh [tag] [reps] ["piece_len:nbuf:GiB ..."]
 set -o pipefail
 R=$GRAFT_REPO_ROOT
@@ -16,7 +17,7 @@ for rep in $(seq 1 $REPS); do
   for c in $CASES; do
     IFS=: read pl nbuf gib <<< "$c"
     for zc in ${ZC_VALUES:-0 1}; do
-      line=$(VX_ZERO_COPY=$zc timeout -k 10 120 ./tools/native/async_probe $pl $nbuf $gib 64 2) || { echo "FAIL pl=$pl zc=$zc"; exit 1; }
+      line=$(VX_ZERO_COPY=$zc timeout -k 10 120 ./tools/native/async_probe $pl $nbuf $gib 64 ${REG:-2}) || { echo "FAIL pl=$pl zc=$zc"; exit 1; }
       echo "{\"zc\": $zc, \"rep\": $rep, \"piece_len\": $pl, \"GiB\": $gib, \"res\": $line}" >> $OUT
     done
   done
