@@ -32,6 +32,10 @@ uint64_t vx_tuning_gather_tiles(const struct vx_ctx* ctx);
  * piece registered and aligned, read from host memory by the hash kernel
  * itself, no gather). */
 uint64_t vx_tuning_zero_copy_slots(const struct vx_ctx* ctx);
+/* 1 if the default policy (VX_ZERO_COPY=2) hashes a slot of n registered,
+ * aligned pieces of total_len bytes with the zero-copy kernel: n >= 128 and a
+ * mean length below 128 KiB or from 512 KiB (host-only). */
+int vx_tuning_zero_copy_plan(uint32_t n, uint64_t total_len);
 /* Fault injection for tests: after k more successful piece submits (async or
  * inside a host batch), the next one fails with VX_ENOMEM without latching
  * the context, as a failed pinned-stage allocation does.  k < 0 turns it off. */

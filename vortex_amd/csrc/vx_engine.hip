@@ -496,12 +496,16 @@ int launch_slot(vx_ctx* c, int si) {
 // from HBM, 6-8 % faster per block than reading host memory as it goes
 // (tools/loop_latency_ab.py: download-loop p50 at 2 / 4 MiB 27.3 / 67.4 ms
 // against 28.8-29.5 / 71.6), so it keeps the gather.
+bool zc_wins(uint32_t n, uint64_t bytes) {
+    if (n < kZcMinPieces) return false;
+    const uint64_t mean = bytes / std::max<uint32_t>(n, 1);
+    return mean < kZcBelow || mean >= kZcFrom;
+}
+
 bool zc_wins(const Slot& s) {
-    if (s.n < kZcMinPieces) return false;
     uint64_t bytes = 0;
     for (uint32_t i = 0; i < s.n; ++i) bytes += s.h_lens[i];
-    const uint64_t mean = bytes / std::max<uint32_t>(s.n, 1);
-    return mean < kZcBelow || mean >= kZcFrom;
+    return zc_wins(s.n, bytes);
 }
 
 int launch_slot_impl(vx_ctx* c, int si) {
@@ -2161,6 +2165,8 @@ uint64_t vx_tuning_chunk_rounds(const vx_ctx* c) { return c ? c->chunk_rounds : 
 uint64_t vx_tuning_gather_tiles(const vx_ctx* c) { return c ? c->gather_tiles : 0; }
 
 uint64_t vx_tuning_zero_copy_slots(const vx_ctx* c) { return c ? c->zero_copy_slots : 0; }
+
+int vx_tuning_zero_copy_plan(uint32_t n, uint64_t total_len) { return zc_wins(n, total_len) ? 1 : 0; }
 int vx_tuning_last_verify(const vx_ctx* c, vx_verify_trace* out) {
     if (!c || !out) return fail(VX_EINVAL, "vx_tuning_last_verify: NULL argument");
     *out = c->last_verify;
