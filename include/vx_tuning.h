@@ -36,6 +36,12 @@ uint64_t vx_tuning_zero_copy_slots(const struct vx_ctx* ctx);
  * aligned pieces of total_len bytes with the zero-copy kernel: n >= 128 and a
  * mean length below 128 KiB or from 512 KiB (host-only). */
 int vx_tuning_zero_copy_plan(uint32_t n, uint64_t total_len);
+/* The zero-copy kernel on its own (A/B probes): piece i is d_lens[i] bytes at
+ * the device-visible address d_srcs[i] (HBM, or a registered host buffer's
+ * device mapping), 16-byte aligned; d_digests n x 20 B, d_expected /
+ * d_matched optional.  Enqueue-only on `stream` (a hipStream_t or NULL). */
+int vx_tuning_zero_copy_kernel(const uint64_t* d_srcs, const uint32_t* d_lens, uint32_t n, void* d_digests,
+                               const void* d_expected, void* d_matched, void* stream);
 /* Fault injection for tests: after k more successful piece submits (async or
  * inside a host batch), the next one fails with VX_ENOMEM without latching
  * the context, as a failed pinned-stage allocation does.  k < 0 turns it off. */

@@ -37,7 +37,7 @@ EXPORTS = (
     "vx_sha1_batch", "vx_verify_batch", "vx_verify_files", "vx_verify_files_range", "vx_verify_files_multi",
     "vx_sha1_device_uniform", "vx_sha1_device_ragged", "vx_sha1_device_ragged_hint", "vx_sort_order",
     "vx_synth_fill", "vx_sha1_device_uniform_variant", "vx_sha1_device_ragged_variant",
-    "vx_tuning_chunk_rounds", "vx_tuning_gather_tiles", "vx_tuning_zero_copy_slots", "vx_tuning_zero_copy_plan", "vx_tuning_plan_ragged", "vx_tuning_chunk_schedule",
+    "vx_tuning_chunk_rounds", "vx_tuning_gather_tiles", "vx_tuning_zero_copy_slots", "vx_tuning_zero_copy_plan", "vx_tuning_zero_copy_kernel", "vx_tuning_plan_ragged", "vx_tuning_chunk_schedule",
     "vx_tuning_fail_submit_after", "vx_plan_verify", "vx_get_stats", "vx_reset_stats",
     "vx_tuning_fail_launch_after", "vx_tuning_last_verify",
 )
@@ -129,6 +129,7 @@ def _declare(L: ctypes.CDLL) -> None:
         "vx_tuning_gather_tiles": ([vp], c.c_uint64),
         "vx_tuning_zero_copy_slots": ([vp], c.c_uint64),
         "vx_tuning_zero_copy_plan": ([c.c_uint32, c.c_uint64], c.c_int),
+        "vx_tuning_zero_copy_kernel": ([vp, vp, c.c_uint32, vp, vp, vp, vp], c.c_int),
         "vx_tuning_fail_submit_after": ([vp, c.c_int64], None),
         "vx_tuning_fail_launch_after": ([vp, c.c_int64], None),
         "vx_tuning_last_verify": ([vp, c.POINTER(vx_verify_trace)], c.c_int),

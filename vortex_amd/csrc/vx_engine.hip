@@ -2167,6 +2167,17 @@ uint64_t vx_tuning_gather_tiles(const vx_ctx* c) { return c ? c->gather_tiles : 
 uint64_t vx_tuning_zero_copy_slots(const vx_ctx* c) { return c ? c->zero_copy_slots : 0; }
 
 int vx_tuning_zero_copy_plan(uint32_t n, uint64_t total_len) { return zc_wins(n, total_len) ? 1 : 0; }
+
+int vx_tuning_zero_copy_kernel(const uint64_t* d_srcs, const uint32_t* d_lens, uint32_t n, void* d_digests,
+                               const void* d_expected, void* d_matched, void* stream) {
+    if (n && (!d_srcs || !d_lens || !d_digests)) return fail(VX_EINVAL, "vx_tuning_zero_copy_kernel: NULL argument");
+    if ((d_expected == nullptr) != (d_matched == nullptr))
+        return fail(VX_EINVAL, "vx_tuning_zero_copy_kernel: expected and matched go together");
+    hipError_t e = vx::launch_zero_copy(d_srcs, d_lens, n, static_cast<uint8_t*>(d_digests),
+                                        static_cast<const uint8_t*>(d_expected), static_cast<uint8_t*>(d_matched),
+                                        static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : hip_fail(e, "vx_tuning_zero_copy_kernel");
+}
 int vx_tuning_last_verify(const vx_ctx* c, vx_verify_trace* out) {
     if (!c || !out) return fail(VX_EINVAL, "vx_tuning_last_verify: NULL argument");
     *out = c->last_verify;
