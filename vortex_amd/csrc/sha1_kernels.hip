@@ -849,6 +849,30 @@ __device__ __forceinline__ void zc_load_tile(uint4 (&r)[16], const uint4 (*ztab)
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// Two of tile t's 16 loads (instructions k0 and k0 + 1): the producer
+// spreads a tile's loads and stage writes over the 8 blocks of the tile
+// before it, so no block carries them all.
+__device__ __forceinline__ void zc_load_pair(uint4 (&r)[16], int k0, const uint4 (*ztab)[64], int lane,
+                                             uint32_t chunk_end, uint64_t t) {
+    const uint64_t o = t * (kZcTileBlocks * 64);
+    const uint64_t zero = reinterpret_cast<uint64_t>(g_zero_line);
+    uint64_t addr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int k = k0 + i;
+        const uint4 e = ztab[k][lane];
+        const uint64_t base = ((uint64_t)e.y << 32) | e.x;
+        addr[i] = o + (k >= 8 ? chunk_end + 256 : chunk_end) <= e.z ? base + o : zero;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const U32x4 v = *reinterpret_cast<GlobalU32x4*>(addr[i]);
+        r[k0 + i] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 template <int S>
 __global__ __launch_bounds__(kPairBlock) void sha1_zc_split_kernel(const uint64_t* __restrict__ srcs,
                                                                    const uint32_t* __restrict__ lens, uint32_t n,
@@ -857,7 +881,7 @@ __global__ __launch_bounds__(kPairBlock) void sha1_zc_split_kernel(const uint64_
                                                                    uint8_t* __restrict__ matched,
                                                                    const uint32_t* __restrict__ exp_index) {
     __shared__ RingLds<S> lds;
-    __shared__ uint4 stage[kZcChunks][kZcPieces];
+    __shared__ uint4 stage[2][kZcChunks][kZcPieces];  // tile t in stage[t & 1]
     __shared__ uint4 ztab[16][64];  // per load instruction and lane: {source lo, hi, full-block bytes, 0}
     __shared__ uint4 padl[4][64];   // each lane's padding block 0 (kept out of VGPRs)
     const int lane = threadIdx.x & 63;
@@ -905,33 +929,47 @@ __global__ __launch_bounds__(kPairBlock) void sha1_zc_split_kernel(const uint64_
         // before it need no select (and no padding words).
         const uint32_t b_sel = __builtin_amdgcn_readfirstlane(wave_min(nfull));
         // Two register tiles in flight (32 KiB per wave; a third measured no
-        // faster, profiles/r03/zero_copy/ab_async_t3.jsonl), as plain arrays
-        // with the tile body written out for each (as a loop over a
-        // ring[2][16], or through a lambda taking the tile by reference,
-        // hipcc kept the tiles in scratch).
+        // faster, profiles/r03/zero_copy/ab_async_t3.jsonl) and two LDS stage
+        // buffers.  While the pair hashes tile t out of stage[t & 1], block bb
+        // writes instructions 2bb, 2bb+1 of tile t+1 (landed in REG) into
+        // stage[(t+1) & 1] and reloads them with tile t+3, so every block
+        // carries the same 2 loads and 2 stage writes (staging a whole tile at
+        // its first block made that block the pair's bound).  Plain arrays and
+        // the tile body written out per register set: as a loop over a
+        // ring[2][16], or through a lambda taking the tile by reference, hipcc
+        // kept the tiles in scratch.
         uint4 ra[16], rb[16];
         zc_load_tile(ra, ztab, lane, chunk_end, 0);
         zc_load_tile(rb, ztab, lane, chunk_end, 1);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t p = 4 * (k & 7) + (lane >> 4), c = c16 + 16 * (k >> 3);
+            stage[0][c][(p + c) & (kZcPieces - 1)] = ra[k];
+        }
+        zc_load_tile(ra, ztab, lane, chunk_end, 2);
         uint32_t w[16];
-        // Stage the landed tile REG, refill REG with tile T + 2, then hash
-        // tile T's (up to) 8 blocks.
-#define VX_ZC_TILE(REG, T)                                                                              \
+        // Tile T from stage[RD]; REG holds tile T+1, staged into stage[1 - RD]
+        // two instructions per block and refilled with tile T+3.  SEL = 0 for a
+        // tile whose blocks are all data for every lane (no per-lane select:
+        // if-converted, the select and its padding reads cost 38 instructions
+        // in EVERY block, profiles/r03/zero_copy/chain_probe.jsonl).
+#define VX_ZC_TILE(REG, T, RD, SEL)                                                                     \
     {                                                                                                   \
         const uint32_t t = (T);                                                                         \
-        _Pragma("unroll") for (int k = 0; k < 16; ++k) {                                                \
-            const uint32_t p = 4 * (k & 7) + (lane >> 4), c = c16 + 16 * (k >> 3);                      \
-            stage[c][(p + c) & (kZcPieces - 1)] = REG[k];                                               \
-        }                                                                                               \
-        zc_load_tile(REG, ztab, lane, chunk_end, t + 2);                                                \
         _Pragma("unroll") for (uint32_t bb = 0; bb < kZcTileBlocks; ++bb) {                             \
+            _Pragma("unroll") for (int k = 2 * bb; k < 2 * (int)bb + 2; ++k) {                          \
+                const uint32_t p = 4 * (k & 7) + (lane >> 4), c = c16 + 16 * (k >> 3);                  \
+                stage[1 - (RD)][c][(p + c) & (kZcPieces - 1)] = REG[k];                                 \
+            }                                                                                           \
+            zc_load_pair(REG, 2 * bb, ztab, lane, chunk_end, t + 3);                                    \
             const uint32_t b = kZcTileBlocks * t + bb;                                                  \
             if (b < nb_wave) { /* wave-uniform */                                                       \
-                const uint4 q0 = stage[4 * bb + 0][(pl + 4 * bb + 0) & (kZcPieces - 1)];                 \
-                const uint4 q1 = stage[4 * bb + 1][(pl + 4 * bb + 1) & (kZcPieces - 1)];                 \
-                const uint4 q2 = stage[4 * bb + 2][(pl + 4 * bb + 2) & (kZcPieces - 1)];                 \
-                const uint4 q3 = stage[4 * bb + 3][(pl + 4 * bb + 3) & (kZcPieces - 1)];                 \
+                const uint4 q0 = stage[RD][4 * bb + 0][(pl + 4 * bb + 0) & (kZcPieces - 1)];             \
+                const uint4 q1 = stage[RD][4 * bb + 1][(pl + 4 * bb + 1) & (kZcPieces - 1)];             \
+                const uint4 q2 = stage[RD][4 * bb + 2][(pl + 4 * bb + 2) & (kZcPieces - 1)];             \
+                const uint4 q3 = stage[RD][4 * bb + 3][(pl + 4 * bb + 3) & (kZcPieces - 1)];             \
                 le_words(w, q0, q1, q2, q3);                                                            \
-                if (b >= b_sel) { /* wave-uniform: some lane is past its data */                        \
+                if (SEL) {                                                                              \
                     const uint4 p0 = padl[0][lane], p1 = padl[1][lane], p2 = padl[2][lane], p3 = padl[3][lane]; \
                     const uint32_t pw[16] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w,            \
                                              p2.x, p2.y, p2.z, p2.w, p3.x, p3.y, p3.z, p3.w};           \
@@ -945,18 +983,21 @@ __global__ __launch_bounds__(kPairBlock) void sha1_zc_split_kernel(const uint64_
                     }                                                                                   \
                 }                                                                                       \
                 expand_store(w, lds.w[ring_slot<S>(b)], lane);                                          \
-                publish<S>(b); /* lgkmcnt(0) + s_barrier: stage reads done before it is rewritten */   \
             }                                                                                           \
+            /* lgkmcnt(0) + s_barrier: this block's stage reads and writes are done before either */   \
+            /* buffer is touched again (the consumer passes one barrier per block it hashes) */        \
+            if (b < nb_wave) publish<S>(b);                                                             \
         }                                                                                               \
     }
         // Straight-line trips (tiles past the data load the zero line, blocks
         // past nb_wave are skipped), so the waitcnt pass sees the same 32
         // loads in flight at the back edge as at the entry and waits for
-        // exactly the 16 of the tile it stages next.
+        // exactly the 2 it stages next; a tile takes the select form only from
+        // the wave's first block that is not data for all lanes.
         const uint32_t ntiles = (nb_wave + kZcTileBlocks - 1) / kZcTileBlocks;
         for (uint32_t t0 = 0; t0 < ntiles; t0 += 2) {
-            VX_ZC_TILE(ra, t0)
-            VX_ZC_TILE(rb, t0 + 1)
+            if (kZcTileBlocks * (t0 + 1) <= b_sel) VX_ZC_TILE(rb, t0, 0, 0) else VX_ZC_TILE(rb, t0, 0, 1)
+            if (kZcTileBlocks * (t0 + 2) <= b_sel) VX_ZC_TILE(ra, t0 + 1, 1, 0) else VX_ZC_TILE(ra, t0 + 1, 1, 1)
         }
 #undef VX_ZC_TILE
         producer_done<S>(nb_wave);
