@@ -30,9 +30,10 @@
 
 namespace vx {
 
-// A 128-byte line of zeros: the load target for lanes that have no full
-// group to stream, so every issued load stays in bounds.
-__device__ __attribute__((aligned(128))) uint4 g_zero_line[8];
+// A line of zeros: the load target for lanes that have no full group to
+// stream, so every issued load stays in bounds (512 bytes: the zero-copy
+// producer adds its 256-byte half offset after choosing it).
+__device__ __attribute__((aligned(128))) uint4 g_zero_line[32];
 
 __device__ __forceinline__ void load_group(uint4 (&dst)[8], const uint4* src) {
 #pragma unroll
@@ -811,9 +812,10 @@ hipError_t launch_chunk(const uint8_t* base, const uint64_t* offsets, const uint
 // async slots leave most CUs idle, and so every piece gets twice the bytes in
 // flight — a tile is 8 blocks (512 B) of all 32 pieces, 16 wave instructions,
 // and two tiles (32 KiB) are in flight per producer wave, 1 KiB per piece.
-// A landed tile is transposed through a 16 KiB LDS stage (chunk c of piece p
-// at [c][(p + c) & 31]: conflict-free both ways) to the lane that owns the
-// piece.  Chunks past a piece's full blocks load the device zero line, so no
+// A landed tile is transposed through a 16.5 KiB LDS stage (chunk c of piece
+// p at [c][p], rows padded to 33 slots: conflict-free both ways, and every
+// access is one base register plus an immediate offset) to the lane that
+// owns the piece.  Chunks past a piece's full blocks load the device zero line, so no
 // load reaches past a piece; the < 64-byte tail and the padding come from the
 // lane's own bytes (tail_words), as in the ragged kernel's phase 2.
 // ---------------------------------------------------------------------------
@@ -824,53 +826,35 @@ constexpr uint32_t kZcChunks = kZcTileBlocks * 4;  // 16-byte chunks per piece p
 typedef uint32_t U32x4 __attribute__((ext_vector_type(4)));
 typedef const __attribute__((address_space(1))) U32x4 GlobalU32x4;
 
-// Tile t's 16 loads: instruction k reads 16 bytes at ztab[k][lane].xy +
-// t*512 (this lane's chunk of its piece) when that chunk lies inside the
-// piece's full blocks (t*512 + chunk_end <= ztab[k][lane].z), else the zero
-// line.  Explicitly global loads: the pointers come from memory, and as flat
-// loads they would also count in lgkmcnt, which every ring barrier drains.
-__device__ __forceinline__ void zc_load_tile(uint4 (&r)[16], const uint4 (*ztab)[64], int lane, uint32_t chunk_end,
-                                             uint64_t t) {
-    const uint64_t o = t * (kZcTileBlocks * 64);
+// Load instruction k of tile t: 16 bytes at zb[k & 7] + t*512 (+256 for
+// the second half, k >= 8) when that chunk lies inside the piece's full
+// blocks (t*512 (+256) < zl[k & 7]), else the zero line.  zb and zl stay in
+// VGPRs: read from LDS they put two dependent LDS round trips in front of
+// every block's loads.  Explicitly global loads: the pointers come from
+// memory, and as flat loads they would also count in lgkmcnt, which every
+// ring barrier drains.
+__device__ __forceinline__ uint4 zc_load(int k, const uint64_t (&zb)[8], const uint32_t (&zl)[8], uint32_t t) {
+    const uint32_t o = t * (kZcTileBlocks * 64) + (k >= 8 ? 256u : 0u);
     const uint64_t zero = reinterpret_cast<uint64_t>(g_zero_line);
-    uint64_t addr[16];
+    const uint64_t a = (o < zl[k & 7] ? zb[k & 7] + t * (kZcTileBlocks * 64) : zero) + (k >= 8 ? 256u : 0u);
+    const U32x4 v = *reinterpret_cast<GlobalU32x4*>(a);  // a native vector load: a uint4 struct copy from AS1
+    return make_uint4(v.x, v.y, v.z, v.w);                 // became a memcpy that kept the tiles in scratch
+}
+
+// All 16 loads of tile t (the prologue).
+__device__ __forceinline__ void zc_load_tile(uint4 (&r)[16], const uint64_t (&zb)[8], const uint32_t (&zl)[8],
+                                             uint32_t t) {
 #pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        const uint4 e = ztab[k][lane];
-        const uint64_t base = ((uint64_t)e.y << 32) | e.x;
-        addr[k] = o + (k >= 8 ? chunk_end + 256 : chunk_end) <= e.z ? base + o : zero;
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {  // a native vector load: a uint4 struct copy from AS1 became a memcpy
-        const U32x4 v = *reinterpret_cast<GlobalU32x4*>(addr[k]);  // that kept the tiles in scratch
-        r[k] = make_uint4(v.x, v.y, v.z, v.w);
-    }
-    __builtin_amdgcn_sched_barrier(0);
+    for (int k = 0; k < 16; ++k) r[k] = zc_load(k, zb, zl, t);
 }
 
 // Two of tile t's 16 loads (instructions k0 and k0 + 1): the producer
 // spreads a tile's loads and stage writes over the 8 blocks of the tile
 // before it, so no block carries them all.
-__device__ __forceinline__ void zc_load_pair(uint4 (&r)[16], int k0, const uint4 (*ztab)[64], int lane,
-                                             uint32_t chunk_end, uint64_t t) {
-    const uint64_t o = t * (kZcTileBlocks * 64);
-    const uint64_t zero = reinterpret_cast<uint64_t>(g_zero_line);
-    uint64_t addr[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int k = k0 + i;
-        const uint4 e = ztab[k][lane];
-        const uint64_t base = ((uint64_t)e.y << 32) | e.x;
-        addr[i] = o + (k >= 8 ? chunk_end + 256 : chunk_end) <= e.z ? base + o : zero;
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const U32x4 v = *reinterpret_cast<GlobalU32x4*>(addr[i]);
-        r[k0 + i] = make_uint4(v.x, v.y, v.z, v.w);
-    }
-    __builtin_amdgcn_sched_barrier(0);
+__device__ __forceinline__ void zc_load_pair(uint4 (&r)[16], int k0, const uint64_t (&zb)[8],
+                                             const uint32_t (&zl)[8], uint32_t t) {
+    r[k0] = zc_load(k0, zb, zl, t);
+    r[k0 + 1] = zc_load(k0 + 1, zb, zl, t);
 }
 
 template <int S>
@@ -881,8 +865,7 @@ __global__ __launch_bounds__(kPairBlock) void sha1_zc_split_kernel(const uint64_
                                                                    uint8_t* __restrict__ matched,
                                                                    const uint32_t* __restrict__ exp_index) {
     __shared__ RingLds<S> lds;
-    __shared__ uint4 stage[2][kZcChunks][kZcPieces];  // tile t in stage[t & 1]
-    __shared__ uint4 ztab[16][64];  // per load instruction and lane: {source lo, hi, full-block bytes, 0}
+    __shared__ uint4 stage[2][kZcChunks][kZcPieces + 1];  // tile t in stage[t & 1]; rows padded to 33 slots
     __shared__ uint4 padl[4][64];   // each lane's padding block 0 (kept out of VGPRs)
     const int lane = threadIdx.x & 63;
     const uint32_t pl = lane & (kZcPieces - 1);  // the piece this lane hashes (lanes 32-63 mirror 0-31)
@@ -900,19 +883,21 @@ __global__ __launch_bounds__(kPairBlock) void sha1_zc_split_kernel(const uint64_
         // ---------------- producer ----------------
         // Load instruction k covers pieces 4(k & 7) .. +3 (16 lanes each) and
         // the (k >> 3)-th 256-byte half of the tile: this lane moves chunk
-        // c16 + 16(k >> 3) of piece 4(k & 7) + (lane >> 4).  The 16
-        // (source, limit) pairs live in LDS, not in 48 VGPRs.
+        // c16 + 16(k >> 3) of piece 4(k & 7) + (lane >> 4), so it keeps one
+        // source and one limit per piece group g = k & 7: the chunk at tile
+        // offset o is data iff o + 16 c16 + 16 <= the piece's full-block
+        // bytes, i.e. o < zl[g].
         const uint32_t c16 = lane & 15;
+        uint64_t zb[8];
+        uint32_t zl[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const uint32_t pk = g0 + 4 * k + (lane >> 4);
+        for (int g = 0; g < 8; ++g) {
+            const uint32_t pk = g0 + 4 * g + (lane >> 4);
             const uint32_t pkk = pk < n ? pk : n - 1;
             const uint32_t full = pk < n ? (lens[pkk] >> 6) * 64u : 0u;
-            const uint64_t base = srcs[pkk] + 16 * c16;
-            ztab[k][lane] = make_uint4((uint32_t)base, (uint32_t)(base >> 32), full, 0u);
-            ztab[k + 8][lane] = make_uint4((uint32_t)(base + 256), (uint32_t)((base + 256) >> 32), full, 0u);
+            zb[g] = srcs[pkk] + 16 * c16;
+            zl[g] = full >= 16 * c16 + 16 ? full - 16 * c16 - 15 : 0u;
         }
-        const uint32_t chunk_end = 16 * c16 + 16;  // (+256 for the second half, zc_load_tile)
         // this lane's padding block 0 (its own tail bytes, read once)
         uint32_t padw[16];
         const uint8_t* q = reinterpret_cast<const uint8_t*>(srcs[jj]) + (size_t)nfull * 64;
@@ -939,14 +924,14 @@ __global__ __launch_bounds__(kPairBlock) void sha1_zc_split_kernel(const uint64_
         // ring[2][16], or through a lambda taking the tile by reference, hipcc
         // kept the tiles in scratch.
         uint4 ra[16], rb[16];
-        zc_load_tile(ra, ztab, lane, chunk_end, 0);
-        zc_load_tile(rb, ztab, lane, chunk_end, 1);
+        zc_load_tile(ra, zb, zl, 0);
+        zc_load_tile(rb, zb, zl, 1);
 #pragma unroll
         for (int k = 0; k < 16; ++k) {
             const uint32_t p = 4 * (k & 7) + (lane >> 4), c = c16 + 16 * (k >> 3);
-            stage[0][c][(p + c) & (kZcPieces - 1)] = ra[k];
+            stage[0][c][p] = ra[k];
         }
-        zc_load_tile(ra, ztab, lane, chunk_end, 2);
+        zc_load_tile(ra, zb, zl, 2);
         uint32_t w[16];
         // Tile T from stage[RD]; REG holds tile T+1, staged into stage[1 - RD]
         // two instructions per block and refilled with tile T+3.  SEL = 0 for a
@@ -959,15 +944,15 @@ __global__ __launch_bounds__(kPairBlock) void sha1_zc_split_kernel(const uint64_
         _Pragma("unroll") for (uint32_t bb = 0; bb < kZcTileBlocks; ++bb) {                             \
             _Pragma("unroll") for (int k = 2 * bb; k < 2 * (int)bb + 2; ++k) {                          \
                 const uint32_t p = 4 * (k & 7) + (lane >> 4), c = c16 + 16 * (k >> 3);                  \
-                stage[1 - (RD)][c][(p + c) & (kZcPieces - 1)] = REG[k];                                 \
+                stage[1 - (RD)][c][p] = REG[k];                                                         \
             }                                                                                           \
-            zc_load_pair(REG, 2 * bb, ztab, lane, chunk_end, t + 3);                                    \
+            zc_load_pair(REG, 2 * bb, zb, zl, t + 3);                                                   \
             const uint32_t b = kZcTileBlocks * t + bb;                                                  \
             if (b < nb_wave) { /* wave-uniform */                                                       \
-                const uint4 q0 = stage[RD][4 * bb + 0][(pl + 4 * bb + 0) & (kZcPieces - 1)];             \
-                const uint4 q1 = stage[RD][4 * bb + 1][(pl + 4 * bb + 1) & (kZcPieces - 1)];             \
-                const uint4 q2 = stage[RD][4 * bb + 2][(pl + 4 * bb + 2) & (kZcPieces - 1)];             \
-                const uint4 q3 = stage[RD][4 * bb + 3][(pl + 4 * bb + 3) & (kZcPieces - 1)];             \
+                const uint4 q0 = stage[RD][4 * bb + 0][pl];                                           \
+                const uint4 q1 = stage[RD][4 * bb + 1][pl];                                           \
+                const uint4 q2 = stage[RD][4 * bb + 2][pl];                                           \
+                const uint4 q3 = stage[RD][4 * bb + 3][pl];                                           \
                 le_words(w, q0, q1, q2, q3);                                                            \
                 if (SEL) {                                                                              \
                     const uint4 p0 = padl[0][lane], p1 = padl[1][lane], p2 = padl[2][lane], p3 = padl[3][lane]; \
