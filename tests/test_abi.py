@@ -153,19 +153,19 @@ def test_ragged_plan_host(built):
 
 
 def test_zero_copy_plan_host(built):
-    """The default zero-copy policy: full async slots of
-    short (< 128 KiB) or long (>= 512 KiB) pieces are hashed from host memory,
-    256 KiB slots and small (latency-bound) batches keep the gather."""
+    """The default zero-copy policy: async slots of at least
+    128 pieces are hashed from host memory whatever their length; small
+    (latency-bound) batches keep the gather."""
     from vortex_amd import _lib
 
     zc = _lib.lib().vx_tuning_zero_copy_plan
     KiB, MiB = 1024, 1 << 20
     assert zc(8192, 8192 * 16 * KiB) == 1       # 16 KiB pieces, a full 128 MiB slot
-    assert zc(512, 512 * 256 * KiB) == 0        # config 1's 256 KiB pieces: gather
+    assert zc(512, 512 * 256 * KiB) == 1        # config 1's 256 KiB pieces
     assert zc(512, 512 * 2 * MiB) == 1          # linux-mint's 2 MiB pieces
-    assert zc(512, 512 * 512 * KiB) == 1 and zc(512, 512 * (512 * KiB - 1)) == 0
-    assert zc(128, 128 * 127 * KiB) == 1 and zc(128, 128 * 128 * KiB) == 0
+    assert zc(128, 128 * 4 * MiB) == 1
     assert zc(127, 127 * 16 * KiB) == 0         # a small batch from the download loop
+    assert zc(32, 32 * 256 * KiB) == 0
     assert zc(0, 0) == 0
 
 

@@ -1,4 +1,4 @@
-"""The zero-copy slot path (VX_ZERO_COPY: 0 never, 1 always, 2 = by mean piece length, the default): a slot whose
+"""The zero-copy slot path (VX_ZERO_COPY: 0 never, 1 always, 2 = slots of >= 128 pieces, the default): a slot whose
 pieces are all registered and 16-byte aligned is hashed straight out of host
 memory by sha1_zc_split_kernel (cooperative 16-lane loads, LDS transpose),
 with no gather kernel.  Every digest and verdict must equal hashlib's / the
@@ -165,13 +165,13 @@ def test_zero_copy_config1_shape(built, gpu, monkeypatch):
         assert got[i][0] == (0 if oracle.is_corrupt(i, every) else 1), i
 
 
-@pytest.mark.parametrize("plen,batch,expect_zc", [(16384, 128, True), (262144, 128, False), (2 << 20, 128, True),
-                                                  (16384, 32, False)])
+@pytest.mark.parametrize("plen,batch,expect_zc", [(16384, 128, True), (262144, 128, True), (2 << 20, 128, True),
+                                                  (16384, 32, False), (262144, 32, False)])
 def test_zero_copy_default_policy(built, gpu, monkeypatch, plen, batch, expect_zc):
     """By default (VX_ZERO_COPY unset = 2) a slot of registered aligned pieces
-    goes zero-copy when it holds at least 128 pieces whose mean length is
-    below 128 KiB or from 512 KiB (vx_engine.hip zc_wins), and through the
-    gather otherwise (small, latency-bound batches included); exact either way."""
+    goes zero-copy when it holds at least 128 pieces (vx_engine.hip zc_wins),
+    and through the gather otherwise (small, latency-bound batches); exact
+    either way."""
     from vortex_amd import _lib
     from vortex_amd.hash_pool import HashPool
 

@@ -69,9 +69,7 @@ int hip_fail(hipError_t e, const char* what) {
     } while (0)
 
 constexpr uint64_t kAlign = 256;
-// zc_wins: the mean piece lengths where gather + hash beats the zero-copy
-// kernel, and the slot size below which a batch is latency-bound
-constexpr uint64_t kZcBelow = 128 * 1024, kZcFrom = 512 * 1024;
+// zc_wins: the slot size below which a batch is latency-bound
 constexpr uint32_t kZcMinPieces = 128;
 
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
@@ -208,7 +206,7 @@ struct vx_ctx {
     // A slot whose pieces are all registered and aligned may be hashed
     // straight out of host memory by the zero-copy kernel, without a gather
     // (sha1_zc_split_kernel).  VX_ZERO_COPY: 0 = never,
-    // 1 = always, 2 = by the slot's mean piece length (zc_wins, default).
+    // 1 = always, 2 = by the slot's piece count (zc_wins, default).
     int zero_copy = 2;
     uint64_t zero_copy_slots = 0;  // slots hashed that way (vx_tuning_zero_copy_slots)
     uint32_t gather_grid = 0;  // VX_GATHER_GRID: workgroups per gather launch (0 = default)
@@ -488,25 +486,15 @@ int launch_slot(vx_ctx* c, int si) {
 }
 
 // Where the zero-copy kernel beats gather + hash (profiles/r03/zero_copy/):
-// on full async slots, by the slot's mean piece length (tools/ab_zero_copy.sh,
+// on full async slots at every piece length measured (tools/ab_zero_copy.sh,
 // alternating runs of async_probe, one registered mmap per buffer): 16 KiB
-// 33 -> 45-48 GiB/s, 1 / 2 / 4 MiB 44 -> 48 / 34 -> 41-44 / 30 -> 35, equal
-// at 64-512 KiB but 1-6 % behind around 256 KiB on a long stream.  A small
-// batch is latency-bound instead: its gather is short and its chain then runs
-// from HBM, 6-8 % faster per block than reading host memory as it goes
-// (tools/loop_latency_ab.py: download-loop p50 at 2 / 4 MiB 27.3 / 67.4 ms
-// against 28.8-29.5 / 71.6), so it keeps the gather.
-bool zc_wins(uint32_t n, uint64_t bytes) {
-    if (n < kZcMinPieces) return false;
-    const uint64_t mean = bytes / std::max<uint32_t>(n, 1);
-    return mean < kZcBelow || mean >= kZcFrom;
-}
-
-bool zc_wins(const Slot& s) {
-    uint64_t bytes = 0;
-    for (uint32_t i = 0; i < s.n; ++i) bytes += s.h_lens[i];
-    return zc_wins(s.n, bytes);
-}
+// 33 -> 48 GiB/s, 256 / 512 KiB 47.8 -> 48.8 / 48.1 -> 49.0, 1 / 2 / 4 MiB
+// 44 -> 48 / 34 -> 44 / 30 -> 35.  A small batch is latency-bound instead:
+// its gather is short and its chain then runs from HBM, ~6 % faster per
+// block than reading host memory as it goes (tools/loop_latency_ab.py,
+// 32-piece batches: download-loop p50 at 256 KiB 3.7 ms against 4.1-4.2, at
+// 2 MiB 27.3-27.7 against 28.2-28.8), so it keeps the gather.
+bool zc_wins(uint32_t n) { return n >= kZcMinPieces; }
 
 int launch_slot_impl(vx_ctx* c, int si) {
     Slot& s = c->slots[si];
@@ -521,7 +509,7 @@ int launch_slot_impl(vx_ctx* c, int si) {
     hipStream_t cs = c->h2d_mode == 3 ? c->copy_stream : s.stream;
     // Zero-copy slot: every piece is read by the hash kernel itself, so no
     // bytes cross PCIe ahead of it and nothing waits for the copy chain.
-    const bool zc = s.gtiles && s.all_mapped && (c->zero_copy == 1 || (c->zero_copy == 2 && zc_wins(s)));
+    const bool zc = s.gtiles && s.all_mapped && (c->zero_copy == 1 || (c->zero_copy == 2 && zc_wins(s.n)));
     stage_copies(s);
     if (!zc)
         if (int rc = chain_h2d(c, si)) return rc;
@@ -2166,7 +2154,10 @@ uint64_t vx_tuning_gather_tiles(const vx_ctx* c) { return c ? c->gather_tiles : 
 
 uint64_t vx_tuning_zero_copy_slots(const vx_ctx* c) { return c ? c->zero_copy_slots : 0; }
 
-int vx_tuning_zero_copy_plan(uint32_t n, uint64_t total_len) { return zc_wins(n, total_len) ? 1 : 0; }
+int vx_tuning_zero_copy_plan(uint32_t n, uint64_t total_len) {
+    (void)total_len;  // the policy no longer depends on the slot's bytes (kept in the signature)
+    return zc_wins(n) ? 1 : 0;
+}
 
 int vx_tuning_zero_copy_kernel(const uint64_t* d_srcs, const uint32_t* d_lens, uint32_t n, void* d_digests,
                                const void* d_expected, void* d_matched, void* stream) {
