@@ -857,13 +857,43 @@ __device__ __forceinline__ void zc_load_pair(uint4 (&r)[16], int k0, const uint6
     r[k0 + 1] = zc_load(k0 + 1, zb, zl, t);
 }
 
-template <int S>
-__global__ __launch_bounds__(kPairBlock) void sha1_zc_split_kernel(const uint64_t* __restrict__ srcs,
-                                                                   const uint32_t* __restrict__ lens, uint32_t n,
-                                                                   uint8_t* __restrict__ digests,
-                                                                   const uint8_t* __restrict__ expected,
-                                                                   uint8_t* __restrict__ matched,
-                                                                   const uint32_t* __restrict__ exp_index) {
+// The loading side's setup: this lane's sources and limits, tiles 0-2 in
+// flight, tile 0 staged.  Load instruction k covers pieces 4(k & 7) .. +3 (16
+// lanes each) and the (k >> 3)-th 256-byte half of the tile: this lane moves
+// chunk c16 + 16(k >> 3) of piece 4(k & 7) + (lane >> 4), so it keeps one
+// source and one limit per piece group g = k & 7: the chunk at tile offset o
+// is data iff o + 16 c16 + 16 <= the piece's full-block bytes, i.e. o < zl[g].
+__device__ __forceinline__ void zc_setup(uint64_t (&zb)[8], uint32_t (&zl)[8], uint4 (&ra)[16], uint4 (&rb)[16],
+                                         uint4 (&stage)[2][kZcChunks][kZcPieces + 1], const uint64_t* srcs,
+                                         const uint32_t* lens, uint32_t n, uint32_t g0, int lane) {
+    const uint32_t c16 = lane & 15;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+        const uint32_t pk = g0 + 4 * g + (lane >> 4);
+        const uint32_t pkk = pk < n ? pk : n - 1;
+        const uint32_t full = pk < n ? (lens[pkk] >> 6) * 64u : 0u;
+        zb[g] = srcs[pkk] + 16 * c16;
+        zl[g] = full >= 16 * c16 + 16 ? full - 16 * c16 - 15 : 0u;
+    }
+    zc_load_tile(ra, zb, zl, 0);
+    zc_load_tile(rb, zb, zl, 1);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const uint32_t p = 4 * (k & 7) + (lane >> 4), c = c16 + 16 * (k >> 3);
+        stage[0][c][p] = ra[k];
+    }
+    zc_load_tile(ra, zb, zl, 2);
+}
+
+// kLoader = false: a pair (consumer wave 0, producer wave 1 that loads,
+// transposes and expands).  kLoader = true: a third wave (2) takes the loads
+// and stage writes, so the expanding producer carries only what the split
+// kernel's producer does; all three pass the same barriers (one extra at the
+// start, once tile 0 is staged).
+template <int S, bool kLoader>
+__global__ __launch_bounds__(kLoader ? 3 * 64 : kPairBlock) void sha1_zc_split_kernel(
+    const uint64_t* __restrict__ srcs, const uint32_t* __restrict__ lens, uint32_t n, uint8_t* __restrict__ digests,
+    const uint8_t* __restrict__ expected, uint8_t* __restrict__ matched, const uint32_t* __restrict__ exp_index) {
     __shared__ RingLds<S> lds;
     __shared__ uint4 stage[2][kZcChunks][kZcPieces + 1];  // tile t in stage[t & 1]; rows padded to 33 slots
     __shared__ uint4 padl[4][64];   // each lane's padding block 0 (kept out of VGPRs)
@@ -878,77 +908,35 @@ __global__ __launch_bounds__(kPairBlock) void sha1_zc_split_kernel(const uint64_
     const uint32_t rem = len & 63u;
     const uint32_t nb = nfull + (rem <= 55 ? 1u : 2u);
     const uint32_t nb_wave = __builtin_amdgcn_readfirstlane(wave_max(nb));
+    const uint32_t c16 = lane & 15;
+    const uint32_t ntiles = (nb_wave + kZcTileBlocks - 1) / kZcTileBlocks;
 
-    if (wave == 1) {
-        // ---------------- producer ----------------
-        // Load instruction k covers pieces 4(k & 7) .. +3 (16 lanes each) and
-        // the (k >> 3)-th 256-byte half of the tile: this lane moves chunk
-        // c16 + 16(k >> 3) of piece 4(k & 7) + (lane >> 4), so it keeps one
-        // source and one limit per piece group g = k & 7: the chunk at tile
-        // offset o is data iff o + 16 c16 + 16 <= the piece's full-block
-        // bytes, i.e. o < zl[g].
-        const uint32_t c16 = lane & 15;
-        uint64_t zb[8];
-        uint32_t zl[8];
-#pragma unroll
-        for (int g = 0; g < 8; ++g) {
-            const uint32_t pk = g0 + 4 * g + (lane >> 4);
-            const uint32_t pkk = pk < n ? pk : n - 1;
-            const uint32_t full = pk < n ? (lens[pkk] >> 6) * 64u : 0u;
-            zb[g] = srcs[pkk] + 16 * c16;
-            zl[g] = full >= 16 * c16 + 16 ? full - 16 * c16 - 15 : 0u;
-        }
-        // this lane's padding block 0 (its own tail bytes, read once)
-        uint32_t padw[16];
-        const uint8_t* q = reinterpret_cast<const uint8_t*>(srcs[jj]) + (size_t)nfull * 64;
-        tail_words(padw, q, rem);
-        const uint32_t bits_hi = (uint32_t)(((uint64_t)len * 8u) >> 32);
-        const uint32_t bits_lo = (uint32_t)((uint64_t)len * 8u);
-        if (rem <= 55) {
-            padw[14] = bits_hi;
-            padw[15] = bits_lo;
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) padl[k][lane] = make_uint4(padw[4 * k], padw[4 * k + 1], padw[4 * k + 2], padw[4 * k + 3]);
-        // The wave's first block that is not data for every lane: blocks
-        // before it need no select (and no padding words).
-        const uint32_t b_sel = __builtin_amdgcn_readfirstlane(wave_min(nfull));
-        // Two register tiles in flight (32 KiB per wave; a third measured no
-        // faster, profiles/r03/zero_copy/ab_async_t3.jsonl) and two LDS stage
-        // buffers.  While the pair hashes tile t out of stage[t & 1], block bb
-        // writes instructions 2bb, 2bb+1 of tile t+1 (landed in REG) into
-        // stage[(t+1) & 1] and reloads them with tile t+3, so every block
-        // carries the same 2 loads and 2 stage writes (staging a whole tile at
-        // its first block made that block the pair's bound).  Plain arrays and
-        // the tile body written out per register set: as a loop over a
-        // ring[2][16], or through a lambda taking the tile by reference, hipcc
-        // kept the tiles in scratch.
-        uint4 ra[16], rb[16];
-        zc_load_tile(ra, zb, zl, 0);
-        zc_load_tile(rb, zb, zl, 1);
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            const uint32_t p = 4 * (k & 7) + (lane >> 4), c = c16 + 16 * (k >> 3);
-            stage[0][c][p] = ra[k];
-        }
-        zc_load_tile(ra, zb, zl, 2);
-        uint32_t w[16];
-        // Tile T from stage[RD]; REG holds tile T+1, staged into stage[1 - RD]
-        // two instructions per block and refilled with tile T+3.  SEL = 0 for a
-        // tile whose blocks are all data for every lane (no per-lane select:
-        // if-converted, the select and its padding reads cost 38 instructions
-        // in EVERY block, profiles/r03/zero_copy/chain_probe.jsonl).
-#define VX_ZC_TILE(REG, T, RD, SEL)                                                                     \
+    // Two register tiles in flight (32 KiB per wave; a third measured no
+    // faster, profiles/r03/zero_copy/ab_async_t3.jsonl) and two LDS stage
+    // buffers.  While the pair hashes tile t out of stage[t & 1], block bb
+    // writes instructions 2bb, 2bb+1 of tile t+1 (landed in REG) into
+    // stage[(t+1) & 1] and reloads them with tile t+3, so every block carries
+    // the same 2 loads and 2 stage writes (staging a whole tile at its first
+    // block made that block the pair's bound).  Plain arrays and the tile body
+    // written out per register set: as a loop over a ring[2][16], or through a
+    // lambda taking the tile by reference, hipcc kept the tiles in scratch.
+    // LOADS: stage and reload; HASH: expand block b from stage[RD].  SEL = 0
+    // for a tile whose blocks are all data for every lane (no per-lane select:
+    // if-converted, the select and its padding reads cost 38 instructions in
+    // EVERY block, profiles/r03/zero_copy/chain_probe.jsonl).
+#define VX_ZC_TILE(REG, T, RD, SEL, LOADS, HASH)                                                        \
     {                                                                                                   \
         const uint32_t t = (T);                                                                         \
         _Pragma("unroll") for (uint32_t bb = 0; bb < kZcTileBlocks; ++bb) {                             \
-            _Pragma("unroll") for (int k = 2 * bb; k < 2 * (int)bb + 2; ++k) {                          \
-                const uint32_t p = 4 * (k & 7) + (lane >> 4), c = c16 + 16 * (k >> 3);                  \
-                stage[1 - (RD)][c][p] = REG[k];                                                         \
+            if (LOADS) {                                                                                \
+                _Pragma("unroll") for (int k = 2 * bb; k < 2 * (int)bb + 2; ++k) {                      \
+                    const uint32_t p = 4 * (k & 7) + (lane >> 4), c = c16 + 16 * (k >> 3);              \
+                    stage[1 - (RD)][c][p] = REG[k];                                                     \
+                }                                                                                       \
+                zc_load_pair(REG, 2 * bb, zb, zl, t + 3);                                               \
             }                                                                                           \
-            zc_load_pair(REG, 2 * bb, zb, zl, t + 3);                                                   \
             const uint32_t b = kZcTileBlocks * t + bb;                                                  \
-            if (b < nb_wave) { /* wave-uniform */                                                       \
+            if ((HASH) && b < nb_wave) { /* wave-uniform */                                             \
                 const uint4 q0 = stage[RD][4 * bb + 0][pl];                                           \
                 const uint4 q1 = stage[RD][4 * bb + 1][pl];                                           \
                 const uint4 q2 = stage[RD][4 * bb + 2][pl];                                           \
@@ -974,33 +962,83 @@ __global__ __launch_bounds__(kPairBlock) void sha1_zc_split_kernel(const uint64_
             if (b < nb_wave) publish<S>(b);                                                             \
         }                                                                                               \
     }
-        // Straight-line trips (tiles past the data load the zero line, blocks
-        // past nb_wave are skipped), so the waitcnt pass sees the same 32
-        // loads in flight at the back edge as at the entry and waits for
-        // exactly the 2 it stages next; a tile takes the select form only from
-        // the wave's first block that is not data for all lanes.
-        const uint32_t ntiles = (nb_wave + kZcTileBlocks - 1) / kZcTileBlocks;
-        for (uint32_t t0 = 0; t0 < ntiles; t0 += 2) {
-            if (kZcTileBlocks * (t0 + 1) <= b_sel) VX_ZC_TILE(rb, t0, 0, 0) else VX_ZC_TILE(rb, t0, 0, 1)
-            if (kZcTileBlocks * (t0 + 2) <= b_sel) VX_ZC_TILE(ra, t0 + 1, 1, 0) else VX_ZC_TILE(ra, t0 + 1, 1, 1)
-        }
-#undef VX_ZC_TILE
-        producer_done<S>(nb_wave);
-    } else {
+    // Straight-line trips (tiles past the data load the zero line, blocks past
+    // nb_wave are skipped), so the waitcnt pass sees the same 32 loads in
+    // flight at the back edge as at the entry and waits for exactly the 2 it
+    // stages next; a tile takes the select form only from the wave's first
+    // block that is not data for all lanes.
+    if (wave == 0) {
         // ---------------- consumer ----------------
         const uint32_t b1 = __builtin_amdgcn_readfirstlane(wave_min(nb));
         State s = iv();
+        if (kLoader) __syncthreads();  // tile 0 staged
         consume<S, true>(s, lds, lane, nb_wave, b1, nb);
         if (lane < (int)kZcPieces && j < n) emit(s, j, digests, expected, matched, exp_index);
+    } else if (kLoader && wave == 2) {
+        // ---------------- loader ----------------
+        uint64_t zb[8];
+        uint32_t zl[8];
+        uint4 ra[16], rb[16];
+        uint32_t w[16];
+        const uint32_t bits_hi = 0, bits_lo = 0;
+        zc_setup(zb, zl, ra, rb, stage, srcs, lens, n, g0, lane);
+        __syncthreads();
+        for (uint32_t t0 = 0; t0 < ntiles; t0 += 2) {
+            VX_ZC_TILE(rb, t0, 0, 0, 1, 0)
+            VX_ZC_TILE(ra, t0 + 1, 1, 0, 1, 0)
+        }
+        (void)w;
+        (void)bits_hi;
+        (void)bits_lo;
+        producer_done<S>(nb_wave);
+    } else {
+        // ---------------- producer ----------------
+        // this lane's padding block 0 (its own tail bytes, read once)
+        uint32_t padw[16];
+        const uint8_t* q = reinterpret_cast<const uint8_t*>(srcs[jj]) + (size_t)nfull * 64;
+        tail_words(padw, q, rem);
+        const uint32_t bits_hi = (uint32_t)(((uint64_t)len * 8u) >> 32);
+        const uint32_t bits_lo = (uint32_t)((uint64_t)len * 8u);
+        if (rem <= 55) {
+            padw[14] = bits_hi;
+            padw[15] = bits_lo;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) padl[k][lane] = make_uint4(padw[4 * k], padw[4 * k + 1], padw[4 * k + 2], padw[4 * k + 3]);
+        // The wave's first block that is not data for every lane: blocks
+        // before it need no select (and no padding words).
+        const uint32_t b_sel = __builtin_amdgcn_readfirstlane(wave_min(nfull));
+        uint64_t zb[8];
+        uint32_t zl[8];
+        uint4 ra[16], rb[16];
+        uint32_t w[16];
+        if (kLoader)
+            __syncthreads();
+        else
+            zc_setup(zb, zl, ra, rb, stage, srcs, lens, n, g0, lane);
+        for (uint32_t t0 = 0; t0 < ntiles; t0 += 2) {
+            if (kZcTileBlocks * (t0 + 1) <= b_sel) VX_ZC_TILE(rb, t0, 0, 0, !kLoader, 1) else VX_ZC_TILE(rb, t0, 0, 1, !kLoader, 1)
+            if (kZcTileBlocks * (t0 + 2) <= b_sel) VX_ZC_TILE(ra, t0 + 1, 1, 0, !kLoader, 1) else VX_ZC_TILE(ra, t0 + 1, 1, 1, !kLoader, 1)
+        }
+        producer_done<S>(nb_wave);
     }
+#undef VX_ZC_TILE
 }
 
 hipError_t launch_zero_copy(const uint64_t* srcs, const uint32_t* lens, uint32_t n, uint8_t* digests,
                             const uint8_t* expected, uint8_t* matched, hipStream_t stream, const uint32_t* exp_index) {
     if (n == 0) return hipSuccess;
     const uint32_t blocks = (n + kZcPieces - 1) / kZcPieces;
-    hipLaunchKernelGGL(sha1_zc_split_kernel<kSplitSlots>, dim3(blocks), dim3(kPairBlock), 0, stream, srcs, lens, n,
-                       digests, expected, matched, exp_index);
+    static const bool loader = [] {  // VX_ZC_LOADER=1: the three-wave form (A/B)
+        const char* e = getenv("VX_ZC_LOADER");
+        return e && e[0] == '1';
+    }();
+    if (loader)
+        hipLaunchKernelGGL((sha1_zc_split_kernel<kSplitSlots, true>), dim3(blocks), dim3(3 * 64), 0, stream, srcs,
+                           lens, n, digests, expected, matched, exp_index);
+    else
+        hipLaunchKernelGGL((sha1_zc_split_kernel<kSplitSlots, false>), dim3(blocks), dim3(kPairBlock), 0, stream,
+                           srcs, lens, n, digests, expected, matched, exp_index);
     return hipGetLastError();
 }
 
