@@ -28,18 +28,21 @@ uint64_t vx_tuning_chunk_rounds(const struct vx_ctx* ctx);
 /* 64 KiB tiles the context's gather kernel has pulled from registered host
  * buffers (async / batch slots). */
 uint64_t vx_tuning_gather_tiles(const struct vx_ctx* ctx);
-/* Slots the context hashed with the zero-copy kernel (VX_ZERO_COPY=1: every
- * piece registered and aligned, read from host memory by the hash kernel
- * itself, no gather). */
+/* Slots the context hashed with the zero-copy kernel (every piece registered
+ * and aligned, read from host memory by the hash kernel itself, no gather;
+ * DESIGN.md §6.5). */
 uint64_t vx_tuning_zero_copy_slots(const struct vx_ctx* ctx);
-/* 1 if the default policy (VX_ZERO_COPY=2) hashes a slot of n registered,
- * aligned pieces of total_len bytes with the zero-copy kernel: n >= 128 and a
- * mean length below 128 KiB or from 512 KiB (host-only). */
+/* How the default policy (VX_ZERO_COPY=2, VX_ZC_LOADER=2) hashes a slot of n
+ * registered, aligned pieces of total_len bytes: 0 gather + hash, 1 the
+ * zero-copy pair, 2 the zero-copy kernel with a loader wave (n < 128, a
+ * latency-bound batch).  Host-only. */
 int vx_tuning_zero_copy_plan(uint32_t n, uint64_t total_len);
 /* The zero-copy kernel on its own (A/B probes): piece i is d_lens[i] bytes at
  * the device-visible address d_srcs[i] (HBM, or a registered host buffer's
  * device mapping), 16-byte aligned; d_digests n x 20 B, d_expected /
- * d_matched optional.  Enqueue-only on `stream` (a hipStream_t or NULL). */
+ * d_matched optional.  The pair form, or with VX_ZC_LOADER=1 in the
+ * environment the three-wave form.  Enqueue-only on `stream` (a hipStream_t
+ * or NULL). */
 int vx_tuning_zero_copy_kernel(const uint64_t* d_srcs, const uint32_t* d_lens, uint32_t n, void* d_digests,
                                const void* d_expected, void* d_matched, void* stream);
 /* Fault injection for tests: after k more successful piece submits (async or

@@ -153,9 +153,10 @@ def test_ragged_plan_host(built):
 
 
 def test_zero_copy_plan_host(built):
-    """The default zero-copy policy: async slots of at least
-    128 pieces are hashed from host memory whatever their length; small
-    (latency-bound) batches keep the gather."""
+    """The default zero-copy policy: every slot of registered
+    aligned pieces is hashed from host memory whatever their length; full
+    slots (>= 128 pieces) by the pair, small (latency-bound) batches by the
+    three-wave form with a loader wave."""
     from vortex_amd import _lib
 
     zc = _lib.lib().vx_tuning_zero_copy_plan
@@ -164,9 +165,9 @@ def test_zero_copy_plan_host(built):
     assert zc(512, 512 * 256 * KiB) == 1        # config 1's 256 KiB pieces
     assert zc(512, 512 * 2 * MiB) == 1          # linux-mint's 2 MiB pieces
     assert zc(128, 128 * 4 * MiB) == 1
-    assert zc(127, 127 * 16 * KiB) == 0         # a small batch from the download loop
-    assert zc(32, 32 * 256 * KiB) == 0
-    assert zc(0, 0) == 0
+    assert zc(127, 127 * 16 * KiB) == 2         # a small batch from the download loop
+    assert zc(32, 32 * 256 * KiB) == 2
+    assert zc(1, 1) == 2
 
 
 def _schedule(L, C, head, tail):

@@ -1,4 +1,4 @@
-"""The zero-copy slot path (VX_ZERO_COPY: 0 never, 1 always, 2 = slots of >= 128 pieces, the default): a slot whose
+"""The zero-copy slot path (VX_ZERO_COPY: 0 never, 1 always, 2 the default policy; VX_ZC_LOADER picks the pair or the three-wave form): a slot whose
 pieces are all registered and 16-byte aligned is hashed straight out of host
 memory by sha1_zc_split_kernel (cooperative 16-lane loads, LDS transpose),
 with no gather kernel.  Every digest and verdict must equal hashlib's / the
@@ -52,11 +52,13 @@ def _run_async(pool, pieces, want, bad_every=9, flush_every=10, table=False):
     return {r.index: (r.hash_matched, r.digest) for r in pool.try_iter()}
 
 
-def test_zero_copy_async_ragged_exact(built, gpu, monkeypatch):
+@pytest.mark.parametrize("loader", ["0", "1"])  # the pair / the three-wave form
+def test_zero_copy_async_ragged_exact(built, gpu, monkeypatch, loader):
     from vortex_amd import _lib
     from vortex_amd.hash_pool import HashPool
 
     monkeypatch.setenv("VX_ZERO_COPY", "1")
+    monkeypatch.setenv("VX_ZC_LOADER", loader)
     lens = EDGE * 5
     random.Random(3).shuffle(lens)
     buf, pieces = _pool_pieces(lens, 11)
@@ -77,13 +79,15 @@ def test_zero_copy_async_ragged_exact(built, gpu, monkeypatch):
     assert zc >= len(pieces) // 40 and tiles == 0  # every slot zero-copy, no gather
 
 
-def test_zero_copy_piece_table_and_batch(built, gpu, monkeypatch):
+@pytest.mark.parametrize("loader", ["0", "1"])
+def test_zero_copy_piece_table_and_batch(built, gpu, monkeypatch, loader):
     """The device piece table (vx_submit_piece) on zero-copy slots, and a
     synchronous batch of short pieces (the slot path of vx_sha1_batch)."""
     from vortex_amd import _lib
     from vortex_amd.hash_pool import HashPool
 
     monkeypatch.setenv("VX_ZERO_COPY", "1")
+    monkeypatch.setenv("VX_ZC_LOADER", loader)
     lens = [65536] * 200 + [1000, 64, 0, 65536 - 7]
     buf, pieces = _pool_pieces(lens, 12)
     want = [hashlib.sha1(p).digest() for p in pieces]
@@ -166,12 +170,11 @@ def test_zero_copy_config1_shape(built, gpu, monkeypatch):
 
 
 @pytest.mark.parametrize("plen,batch,expect_zc", [(16384, 128, True), (262144, 128, True), (2 << 20, 128, True),
-                                                  (16384, 32, False), (262144, 32, False)])
+                                                  (16384, 32, True), (262144, 32, True)])
 def test_zero_copy_default_policy(built, gpu, monkeypatch, plen, batch, expect_zc):
     """By default (VX_ZERO_COPY unset = 2) a slot of registered aligned pieces
-    goes zero-copy when it holds at least 128 pieces (vx_engine.hip zc_wins),
-    and through the gather otherwise (small, latency-bound batches); exact
-    either way."""
+    goes zero-copy at every length and batch size (vx_engine.hip zc_wins;
+    small batches in the three-wave form) and never touches the gather."""
     from vortex_amd import _lib
     from vortex_amd.hash_pool import HashPool
 

@@ -1026,13 +1026,10 @@ __global__ __launch_bounds__(kLoader ? 3 * 64 : kPairBlock) void sha1_zc_split_k
 }
 
 hipError_t launch_zero_copy(const uint64_t* srcs, const uint32_t* lens, uint32_t n, uint8_t* digests,
-                            const uint8_t* expected, uint8_t* matched, hipStream_t stream, const uint32_t* exp_index) {
+                            const uint8_t* expected, uint8_t* matched, bool loader, hipStream_t stream,
+                            const uint32_t* exp_index) {
     if (n == 0) return hipSuccess;
     const uint32_t blocks = (n + kZcPieces - 1) / kZcPieces;
-    static const bool loader = [] {  // VX_ZC_LOADER=1: the three-wave form (A/B)
-        const char* e = getenv("VX_ZC_LOADER");
-        return e && e[0] == '1';
-    }();
     if (loader)
         hipLaunchKernelGGL((sha1_zc_split_kernel<kSplitSlots, true>), dim3(blocks), dim3(3 * 64), 0, stream, srcs,
                            lens, n, digests, expected, matched, exp_index);

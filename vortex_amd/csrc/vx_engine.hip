@@ -208,6 +208,9 @@ struct vx_ctx {
     // (sha1_zc_split_kernel).  VX_ZERO_COPY: 0 = never,
     // 1 = always, 2 = by the slot's piece count (zc_wins, default).
     int zero_copy = 2;
+    // The zero-copy kernel's form (zc_loader_wins): VX_ZC_LOADER 0 = the
+    // pair, 1 = with a loader wave, 2 = by the slot's piece count (default).
+    int zc_loader = 2;
     uint64_t zero_copy_slots = 0;  // slots hashed that way (vx_tuning_zero_copy_slots)
     uint32_t gather_grid = 0;  // VX_GATHER_GRID: workgroups per gather launch (0 = default)
     uint64_t gather_tiles = 0;  // tiles gathered (vx_tuning_gather_tiles)
@@ -486,15 +489,24 @@ int launch_slot(vx_ctx* c, int si) {
 }
 
 // Where the zero-copy kernel beats gather + hash (profiles/r03/zero_copy/):
-// on full async slots at every piece length measured (tools/ab_zero_copy.sh,
-// alternating runs of async_probe, one registered mmap per buffer): 16 KiB
-// 33 -> 48 GiB/s, 256 / 512 KiB 47.8 -> 48.8 / 48.1 -> 49.0, 1 / 2 / 4 MiB
-// 44 -> 48 / 34 -> 44 / 30 -> 35.  A small batch is latency-bound instead:
-// its gather is short and its chain then runs from HBM, ~6 % faster per
-// block than reading host memory as it goes (tools/loop_latency_ab.py,
-// 32-piece batches: download-loop p50 at 256 KiB 3.7 ms against 4.1-4.2, at
-// 2 MiB 27.3-27.7 against 28.2-28.8), so it keeps the gather.
-bool zc_wins(uint32_t n) { return n >= kZcMinPieces; }
+// everywhere measured.  Full async slots (tools/ab_zero_copy.sh, alternating
+// runs of async_probe, one registered mmap per buffer): 16 KiB 33 -> 48
+// GiB/s, 256 / 512 KiB 47.8 -> 48.8 / 48.1 -> 49.0, 1 / 2 / 4 MiB 44 -> 48 /
+// 34 -> 44 / 30 -> 35.  Small, latency-bound batches (tools/loop_latency_ab.py,
+// 32-piece batches) only in the three-wave form: download-loop p50 at 32 KiB
+// 0.68 ms against 0.70, 256 KiB 3.75 against 3.75, 2 MiB 26.6 against 27.7.
+bool zc_wins(uint32_t n) {
+    (void)n;
+    return true;
+}
+
+// The loader wave takes the loads off the producer, so the chain reading host
+// memory runs at 0.78 us per block instead of 0.83-0.86 (tools/zc_chain_probe
+// .py): latency-bound batches then finish 7-9 % sooner (p50 at 256 KiB 3.75
+// ms against 4.13, 2 MiB 26.7 against 28.8).  On full slots, where PCIe
+// binds, it ran 2-4 % behind the pair (256 KiB streamed 49.1 against 50.9
+// GiB/s; ab_loader3.jsonl), so those keep the pair.
+bool zc_loader_wins(uint32_t n) { return n < kZcMinPieces; }
 
 int launch_slot_impl(vx_ctx* c, int si) {
     Slot& s = c->slots[si];
@@ -550,7 +562,8 @@ int launch_slot_impl(vx_ctx* c, int si) {
     mark_launched(c, si);
     hipError_t e;
     if (zc) {
-        e = vx::launch_zero_copy(s.d_src, s.d_lens, n, s.d_digests, d_exp, s.d_matched, s.stream, d_row);
+        const bool loader = c->zc_loader == 1 || (c->zc_loader == 2 && zc_loader_wins(n));
+        e = vx::launch_zero_copy(s.d_src, s.d_lens, n, s.d_digests, d_exp, s.d_matched, loader, s.stream, d_row);
         c->zero_copy_slots++;
     } else if (s.uniform) {
         const uint32_t len = s.h_lens[0];
@@ -821,6 +834,7 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (const char* m = std::getenv("VX_GATHER")) c->gather = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_GATHER_GRID")) c->gather_grid = (uint32_t)std::atoi(m);
     if (const char* m = std::getenv("VX_ZERO_COPY")) c->zero_copy = std::max(0, std::min(2, std::atoi(m)));
+    if (const char* m = std::getenv("VX_ZC_LOADER")) c->zc_loader = std::max(0, std::min(2, std::atoi(m)));
     if (const char* m = std::getenv("VX_LAZY_FLUSH")) c->lazy_flush = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_BATCH_SORT")) c->batch_sort = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_BATCH_CHUNK")) c->batch_chunk = align_up(std::strtoull(m, nullptr, 0), kAlign);
@@ -2156,7 +2170,7 @@ uint64_t vx_tuning_zero_copy_slots(const vx_ctx* c) { return c ? c->zero_copy_sl
 
 int vx_tuning_zero_copy_plan(uint32_t n, uint64_t total_len) {
     (void)total_len;  // the policy no longer depends on the slot's bytes (kept in the signature)
-    return zc_wins(n) ? 1 : 0;
+    return zc_wins(n) ? (zc_loader_wins(n) ? 2 : 1) : 0;
 }
 
 int vx_tuning_zero_copy_kernel(const uint64_t* d_srcs, const uint32_t* d_lens, uint32_t n, void* d_digests,
@@ -2164,9 +2178,10 @@ int vx_tuning_zero_copy_kernel(const uint64_t* d_srcs, const uint32_t* d_lens, u
     if (n && (!d_srcs || !d_lens || !d_digests)) return fail(VX_EINVAL, "vx_tuning_zero_copy_kernel: NULL argument");
     if ((d_expected == nullptr) != (d_matched == nullptr))
         return fail(VX_EINVAL, "vx_tuning_zero_copy_kernel: expected and matched go together");
+    const char* l = std::getenv("VX_ZC_LOADER");  // 1: the three-wave form
     hipError_t e = vx::launch_zero_copy(d_srcs, d_lens, n, static_cast<uint8_t*>(d_digests),
                                         static_cast<const uint8_t*>(d_expected), static_cast<uint8_t*>(d_matched),
-                                        static_cast<hipStream_t>(stream));
+                                        l && l[0] == '1', static_cast<hipStream_t>(stream));
     return e == hipSuccess ? 0 : hip_fail(e, "vx_tuning_zero_copy_kernel");
 }
 int vx_tuning_last_verify(const vx_ctx* c, vx_verify_trace* out) {

@@ -76,9 +76,10 @@ hipError_t launch_gather(const uint64_t* src, const uint64_t* dst_off, const uin
 // Zero-copy split kernel: piece i is read straight from
 // registered host memory at its device-mapped address srcs[i] (16-byte
 // aligned, lens[i] bytes; srcs[i] may be 0 when lens[i] == 0); digests /
-// matched row i (expected row exp_index[i] when given).
+// matched row i (expected row exp_index[i] when given).  loader: the
+// three-wave form (a loader wave beside producer and consumer).
 hipError_t launch_zero_copy(const uint64_t* srcs, const uint32_t* lens, uint32_t n, uint8_t* digests,
-                            const uint8_t* expected, uint8_t* matched, hipStream_t stream,
+                            const uint8_t* expected, uint8_t* matched, bool loader, hipStream_t stream,
                             const uint32_t* exp_index = nullptr);
 
 hipError_t launch_synth_fill(uint8_t* base, uint64_t stride, uint32_t len, uint32_t n, uint64_t first,
