@@ -32,10 +32,11 @@ uint64_t vx_tuning_gather_tiles(const struct vx_ctx* ctx);
  * and aligned, read from host memory by the hash kernel itself, no gather;
  * DESIGN.md §6.5). */
 uint64_t vx_tuning_zero_copy_slots(const struct vx_ctx* ctx);
-/* How the default policy (VX_ZERO_COPY=2, VX_ZC_LOADER=2) hashes a slot of n
- * registered, aligned pieces of total_len bytes: 0 gather + hash, 1 the
- * zero-copy pair, 2 the zero-copy kernel with a loader wave (n < 128, a
- * latency-bound batch).  Host-only. */
+/* How the default policy (VX_ZERO_COPY unset, VX_ZC_LOADER=2) hashes a slot
+ * of n registered, aligned pieces of total_len bytes: 1 the zero-copy pair,
+ * 2 the zero-copy kernel with a loader wave (n < 128, a latency-bound batch);
+ * 0 (gather + hash) is only taken with VX_ZERO_COPY=0.  Host-only
+ * (DESIGN.md §6.5). */
 int vx_tuning_zero_copy_plan(uint32_t n, uint64_t total_len);
 /* The zero-copy kernel on its own (A/B probes): piece i is d_lens[i] bytes at
  * the device-visible address d_srcs[i] (HBM, or a registered host buffer's

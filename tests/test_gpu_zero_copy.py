@@ -1,4 +1,4 @@
-"""The zero-copy slot path (VX_ZERO_COPY: 0 never, 1 always, 2 the default policy; VX_ZC_LOADER picks the pair or the three-wave form): a slot whose
+"""The zero-copy slot path (VX_ZERO_COPY=0 turns it off, anything else is the default; VX_ZC_LOADER picks the pair or the three-wave form): a slot whose
 pieces are all registered and 16-byte aligned is hashed straight out of host
 memory by sha1_zc_split_kernel (cooperative 16-lane loads, LDS transpose),
 with no gather kernel.  Every digest and verdict must equal hashlib's / the
@@ -172,8 +172,8 @@ def test_zero_copy_config1_shape(built, gpu, monkeypatch):
 @pytest.mark.parametrize("plen,batch,expect_zc", [(16384, 128, True), (262144, 128, True), (2 << 20, 128, True),
                                                   (16384, 32, True), (262144, 32, True)])
 def test_zero_copy_default_policy(built, gpu, monkeypatch, plen, batch, expect_zc):
-    """By default (VX_ZERO_COPY unset = 2) a slot of registered aligned pieces
-    goes zero-copy at every length and batch size (vx_engine.hip zc_wins;
+    """By default (VX_ZERO_COPY unset) a slot of registered aligned pieces
+    goes zero-copy at every length and batch size (vx_engine.hip launch_slot_impl;
     small batches in the three-wave form) and never touches the gather."""
     from vortex_amd import _lib
     from vortex_amd.hash_pool import HashPool

@@ -19,7 +19,7 @@ sys.path.insert(0, ROOT)
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=2)
-    ap.add_argument("--values", default="0,1", help="VX_ZERO_COPY values to alternate (2 = the default policy)")
+    ap.add_argument("--values", default="0,1", help="VX_ZERO_COPY values to alternate (anything but 0 = the default)")
     a = ap.parse_args()
     import oracle
 

@@ -69,7 +69,7 @@ int hip_fail(hipError_t e, const char* what) {
     } while (0)
 
 constexpr uint64_t kAlign = 256;
-// zc_wins: the slot size below which a batch is latency-bound
+// zc_loader_wins: the slot size below which a batch is latency-bound
 constexpr uint32_t kZcMinPieces = 128;
 
 uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
@@ -205,9 +205,9 @@ struct vx_ctx {
     bool gather = true;        // VX_GATHER=0 turns the gather kernel off (A/B)
     // A slot whose pieces are all registered and aligned may be hashed
     // straight out of host memory by the zero-copy kernel, without a gather
-    // (sha1_zc_split_kernel).  VX_ZERO_COPY: 0 = never,
-    // 1 = always, 2 = by the slot's piece count (zc_wins, default).
-    int zero_copy = 2;
+    // (sha1_zc_split_kernel).  VX_ZERO_COPY=0 turns it off
+    // (A/B); any other value, and the default, takes every eligible slot.
+    bool zero_copy = true;
     // The zero-copy kernel's form (zc_loader_wins): VX_ZC_LOADER 0 = the
     // pair, 1 = with a loader wave, 2 = by the slot's piece count (default).
     int zc_loader = 2;
@@ -488,17 +488,13 @@ int launch_slot(vx_ctx* c, int si) {
     return rc;
 }
 
-// Where the zero-copy kernel beats gather + hash (profiles/r03/zero_copy/):
-// everywhere measured.  Full async slots (tools/ab_zero_copy.sh, alternating
+// Every eligible slot goes zero-copy: the kernel beats gather + hash
+// everywhere measured (profiles/r03/zero_copy/).  Full async slots (tools/ab_zero_copy.sh, alternating
 // runs of async_probe, one registered mmap per buffer): 16 KiB 33 -> 48
 // GiB/s, 256 / 512 KiB 47.8 -> 48.8 / 48.1 -> 49.0, 1 / 2 / 4 MiB 44 -> 48 /
 // 34 -> 44 / 30 -> 35.  Small, latency-bound batches (tools/loop_latency_ab.py,
 // 32-piece batches) only in the three-wave form: download-loop p50 at 32 KiB
 // 0.68 ms against 0.70, 256 KiB 3.75 against 3.75, 2 MiB 26.6 against 27.7.
-bool zc_wins(uint32_t n) {
-    (void)n;
-    return true;
-}
 
 // The loader wave takes the loads off the producer, so the chain reading host
 // memory runs at 0.78 us per block instead of 0.83-0.86 (tools/zc_chain_probe
@@ -521,7 +517,7 @@ int launch_slot_impl(vx_ctx* c, int si) {
     hipStream_t cs = c->h2d_mode == 3 ? c->copy_stream : s.stream;
     // Zero-copy slot: every piece is read by the hash kernel itself, so no
     // bytes cross PCIe ahead of it and nothing waits for the copy chain.
-    const bool zc = s.gtiles && s.all_mapped && (c->zero_copy == 1 || (c->zero_copy == 2 && zc_wins(s.n)));
+    const bool zc = s.gtiles && s.all_mapped && c->zero_copy;
     stage_copies(s);
     if (!zc)
         if (int rc = chain_h2d(c, si)) return rc;
@@ -833,7 +829,7 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (const char* m = std::getenv("VX_H2D_MODE")) c->h2d_mode = std::atoi(m) & 3;
     if (const char* m = std::getenv("VX_GATHER")) c->gather = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_GATHER_GRID")) c->gather_grid = (uint32_t)std::atoi(m);
-    if (const char* m = std::getenv("VX_ZERO_COPY")) c->zero_copy = std::max(0, std::min(2, std::atoi(m)));
+    if (const char* m = std::getenv("VX_ZERO_COPY")) c->zero_copy = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_ZC_LOADER")) c->zc_loader = std::max(0, std::min(2, std::atoi(m)));
     if (const char* m = std::getenv("VX_LAZY_FLUSH")) c->lazy_flush = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_BATCH_SORT")) c->batch_sort = std::atoi(m) != 0;
@@ -2170,7 +2166,7 @@ uint64_t vx_tuning_zero_copy_slots(const vx_ctx* c) { return c ? c->zero_copy_sl
 
 int vx_tuning_zero_copy_plan(uint32_t n, uint64_t total_len) {
     (void)total_len;  // the policy no longer depends on the slot's bytes (kept in the signature)
-    return zc_wins(n) ? (zc_loader_wins(n) ? 2 : 1) : 0;
+    return zc_loader_wins(n) ? 2 : 1;
 }
 
 int vx_tuning_zero_copy_kernel(const uint64_t* d_srcs, const uint32_t* d_lens, uint32_t n, void* d_digests,
