@@ -10,6 +10,8 @@ line per configuration with the GiB/s runs and each call's
 vx_tuning_last_verify budget, and the CPU pool on the same file.
 
 usage: python tools/reverify_ab.py [--reps 3] [--cold-reps 2] [--configs name=K=V,K=V;...]
+A configuration's IO_THREADS=N (not an engine knob) sets its io_threads
+(default: the process's CPU share).
 """
 import argparse
 import json
@@ -56,7 +58,9 @@ def main():
     path = os.path.join(d, f"vx_ab_linuxmint_{os.getpid()}.iso")
     buf = ctypes.create_string_buffer(pl)
     configs = parse(a.configs)
-    res = {name: {"warm": [], "cold": [], "warm_tr": [], "cold_tr": [], "env": env} for name, env in configs}
+    io = {name: int(env.pop("IO_THREADS", 0)) or threads for name, env in configs}
+    res = {name: {"warm": [], "cold": [], "warm_tr": [], "cold_tr": [], "env": env, "io_threads": io[name]}
+           for name, env in configs}
     cpu = {"warm": [], "cold": []}
     try:
         with open(path, "wb") as f:
@@ -78,7 +82,7 @@ def main():
                     os.environ.pop(k, None)
                 else:
                     os.environ[k] = v
-            got, bad = pools[name].verify_files([path], [total], pl, exp, io_threads=threads)  # warm-up
+            got, bad = pools[name].verify_files([path], [total], pl, exp, io_threads=io[name])  # warm-up
             assert all(got) and bad == 0
         for leg, reps in (("warm", a.reps), ("cold", a.cold_reps)):
             for _ in range(reps):
@@ -86,7 +90,7 @@ def main():
                     if leg == "cold":
                         bench.drop_cache(path)
                     t0 = time.perf_counter()
-                    got, bad = pools[name].verify_files([path], [total], pl, exp, io_threads=threads)
+                    got, bad = pools[name].verify_files([path], [total], pl, exp, io_threads=io[name])
                     el = time.perf_counter() - t0
                     assert all(got) and bad == 0
                     res[name][leg].append(round(total / el / (1 << 30), 2))
