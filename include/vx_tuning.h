@@ -81,6 +81,7 @@ typedef struct vx_verify_trace {
     uint32_t readers;      /* reader threads                                          */
     uint32_t rounds;       /* timed copies (chunk rounds)                             */
     uint64_t direct_bytes; /* of read_bytes, read with O_DIRECT (not cached; §6.1)    */
+    uint64_t chunk_bytes;  /* chunk of the resumable rounds (0: whole-piece slots)    */
 } vx_verify_trace;
 int vx_tuning_last_verify(const struct vx_ctx* ctx, vx_verify_trace* out);
 

@@ -6,7 +6,8 @@
 // and not, aligned and unaligned destinations, a range ending at EOF, an
 // aligned head with an unaligned tail — through DirectIo::read into a
 // page-aligned buffer, and compares each with a plain buffered pread.  Prints
-// {"reads": n, "mismatches": k, "direct_bytes": b}.
+// {"reads": n, "mismatches": k, "direct_bytes": b, "resident": f}, f being
+// DirectIo::resident_fraction() sampled before any read.
 #include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -32,6 +33,7 @@ int main(int argc, char** argv) {
     std::vector<int> fds{fd};
     const char* paths[1] = {path};
     vx_files::DirectIo dio(paths, fds, mode);
+    const double resident = dio.resident_fraction();
     const int64_t K = 4096;
     struct R {
         int64_t off, len, dst_skew;
@@ -53,8 +55,8 @@ int main(int argc, char** argv) {
         const bool okb = vx_files::read_full(fd, b.data(), r.off, r.len);
         if (!ok || !okb || std::memcmp(a + r.dst_skew, b.data(), (size_t)r.len) != 0) ++mism;
     }
-    std::printf("{\"reads\": %d, \"mismatches\": %d, \"direct_bytes\": %llu}\n", n, mism,
-                (unsigned long long)dio.direct_bytes());
+    std::printf("{\"reads\": %d, \"mismatches\": %d, \"direct_bytes\": %llu, \"resident\": %.4f}\n", n, mism,
+                (unsigned long long)dio.direct_bytes(), resident);
     free(a);
     close(fd);
     return 0;

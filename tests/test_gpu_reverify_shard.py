@@ -161,14 +161,16 @@ def test_verify_files_multi_contexts(built, gpu, tmp_path, nctx, pl):
             p.close()
 
 
-@pytest.mark.parametrize("pl", [256 * 1024, 2 << 20])  # whole-piece slots / resumable chunk rounds
-def test_verify_files_cold_direct_reads(built, gpu, tmp_path, pl):
+@pytest.mark.parametrize("pl,cold_chunk", [(256 * 1024, 0), (2 << 20, 0), (2 << 20, 1 << 20), (4 << 20, 1 << 20)])
+def test_verify_files_cold_direct_reads(built, gpu, tmp_path, monkeypatch, pl, cold_chunk):
     """Re-verify of files whose pages are NOT in the page cache: the readers
     take the O_DIRECT path for aligned, uncached ranges (vx_files::DirectIo,
     DESIGN.md §6.1) and the buffered path for the rest (unaligned segments
     where files meet, a short tail).  Verdicts equal the oracle's on the same
     damaged multi-file torrent, and the call's trace shows direct reads when
-    the filesystem takes O_DIRECT."""
+    the filesystem takes O_DIRECT.  With VX_VERIFY_COLD_CHUNK (off by
+    default) evicted calls of pieces >= 2 MiB run 1 MiB rounds (many windows
+    of the 16 MiB slots); cached ones, and every call by default, 256 KiB."""
     from vortex_amd.hash_pool import HashPool
 
     d = str(tmp_path)
@@ -195,6 +197,11 @@ def test_verify_files_cold_direct_reads(built, gpu, tmp_path, pl):
             os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
             os.close(fd)
 
+    if cold_chunk:
+        monkeypatch.setenv("VX_VERIFY_COLD_CHUNK", str(cold_chunk))
+    else:
+        monkeypatch.delenv("VX_VERIFY_COLD_CHUNK", raising=False)
+    chunked = pl >= 2 << 20
     with HashPool(pl, slots=3, slot_bytes=16 << 20) as pool:
         for _ in range(2):
             evict()
@@ -204,10 +211,13 @@ def test_verify_files_cold_direct_reads(built, gpu, tmp_path, pl):
             assert tr["read_bytes"] == sum(sizes)
             if direct_ok:
                 assert tr["direct_bytes"] > 0
+                assert tr["chunk_bytes"] == ((cold_chunk or 256 * 1024) if chunked else 0), tr
         # cached now (the buffered reads above filled part of it; read the rest): no direct reads
         for p in paths:
             with open(p, "rb") as f:
                 while f.read(1 << 20):
                     pass
         got, bad = pool.verify_files(paths, sizes, pl, exp, io_threads=4)
-        assert got == want and pool.last_verify()["direct_bytes"] == 0
+        tr = pool.last_verify()
+        assert got == want and tr["direct_bytes"] == 0
+        assert tr["chunk_bytes"] == (256 * 1024 if chunked else 0), tr

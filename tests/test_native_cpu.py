@@ -115,7 +115,9 @@ def test_direct_reads_of_uncached_ranges(tmp_path):
     """vx_files::DirectIo (the re-verify's O_DIRECT path, DESIGN.md §6.1):
     every read returns the file's bytes whatever the alignment; ranges not in
     the page cache go O_DIRECT (mode 1: mincore probe; mode 3: RWF_NOWAIT
-    read first) and cached ones do not; mode 0 never, mode 2 whenever aligned."""
+    read first) and cached ones do not; mode 0 never, mode 2 whenever aligned.
+    resident_fraction (which picks the re-verify's cold chunk) is ~0 on the
+    evicted file, 1 on the cached one, and 1 when nothing is mapped (mode 0)."""
     d = _disk_dir(tmp_path)
     if d is None:
         pytest.skip("no filesystem here takes O_DIRECT")
@@ -141,11 +143,15 @@ def test_direct_reads_of_uncached_ranges(tmp_path):
             out = subprocess.run([str(exe), path, str(mode)], capture_output=True, text=True, check=True, timeout=60)
             res = json.loads(out.stdout)
             assert res["reads"] >= 9 and res["mismatches"] == 0, res
+            resident.append(res["resident"])
             return res["direct_bytes"]
 
-        assert run(0, evict=True) == 0
+        resident = []
+        assert run(0, evict=True) == 0 and resident[-1] == 1.0  # nothing mapped: the warm choice stands
         cold = run(1, evict=True)
+        assert resident[-1] < 0.5, resident  # the kernel may keep a few pages
         warm = run(1, evict=False)
+        assert resident[-1] == 1.0
         assert warm == 0  # cached: buffered
         forced = run(2, evict=False)
         assert forced > 0

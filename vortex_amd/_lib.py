@@ -81,7 +81,8 @@ class vx_verify_trace(ctypes.Structure):
     _fields_ = [(name, ctypes.c_double) for name in (
         "wall_ms", "read_busy_ms", "read_span_ms", "first_read_ms", "copy_busy_ms", "copy_span_ms", "tail_ms")] + [
         ("read_bytes", ctypes.c_uint64), ("copy_bytes", ctypes.c_uint64), ("readers", ctypes.c_uint32),
-        ("rounds", ctypes.c_uint32), ("direct_bytes", ctypes.c_uint64)]
+        ("rounds", ctypes.c_uint32), ("direct_bytes", ctypes.c_uint64),
+        ("chunk_bytes", ctypes.c_uint64)]
 
 
 _lib = None

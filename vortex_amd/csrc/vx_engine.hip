@@ -157,6 +157,15 @@ struct vx_ctx {
     // and the piece length above which it chunks (0 = pieces >= 2 chunks).
     // Env overrides: VX_VERIFY_CHUNK, VX_VERIFY_RAMP, VX_VERIFY_CHUNKED_ABOVE.
     uint64_t verify_chunk = 0;
+    // Chunk bytes when the torrent's data is not in the page cache
+    // (DirectIo::resident_fraction < 0.5 at the call's start), where the
+    // readers go O_DIRECT and the disk binds; warm calls keep
+    // verify_chunk_for's choice.  Off by default (VX_VERIFY_COLD_CHUNK=N
+    // turns it on): 1 MiB cold chunks measured +57 % and +7 % on two boxes
+    // but -2 % and -5 % (median of 6 and 10 evicted calls) on two more, 512
+    // KiB +4 % (profiles/r03/cold/ab_chunk_box*.jsonl, ab_cold_chunk_box*.jsonl):
+    // the box's disk decides, not the chunk.
+    uint64_t verify_cold_chunk = 0;
     int verify_ramp = 1;  // ramp depth d: first/last rounds C / 2^(d+1) (0 = off)
     int verify_ramp_growth = 0;  // head ramp: 0 = rounds double, 1 = grow x5/4 (VX_VERIFY_RAMP_GROWTH)
     uint64_t verify_chunked_above = 0;
@@ -842,6 +851,10 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (const char* m = std::getenv("VX_VERIFY_OVERLAP")) c->verify_overlap = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_VERIFY_COALESCE")) c->verify_coalesce = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_VERIFY_READAHEAD")) c->verify_readahead = (uint32_t)std::max(1, std::atoi(m));
+    if (const char* m = std::getenv("VX_VERIFY_COLD_CHUNK")) {
+        const uint64_t v = std::strtoull(m, nullptr, 0);
+        c->verify_cold_chunk = v ? std::max<uint64_t>(4096, align_up(v, 4096)) : 0;
+    }
     if (const char* m = std::getenv("VX_VERIFY_DIRECT")) c->verify_direct = std::max(0, std::min(3, std::atoi(m)));
     if (const char* m = std::getenv("VX_VERIFY_NUMA")) c->verify_numa = std::atoi(m) != 0;
     if (const char* m = std::getenv("VX_VERIFY_HELPERS")) c->verify_helpers = std::max(0, std::min(16, std::atoi(m)));
@@ -1950,7 +1963,15 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
                              c->verify_direct ? c->verify_helpers : 0);
         FileVerify fv{c, expected, matched_out, bad};
         c->harvest_counts_mismatches = false;
-        rc = chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total, first, end, C)
+        // Uncached data: the disk binds, and takes bigger reads better.
+        const uint64_t Cc = c->verify_cold_chunk;
+        const uint64_t Cv = chunked && !c->verify_chunk && c->verify_direct && Cc > C &&
+                                    piece_length >= 2 * Cc && c->slots[0].arena_cap >= Cc &&
+                                    dio.resident_fraction() < 0.5
+                                ? Cc
+                                : C;
+        c->last_verify.chunk_bytes = chunked ? Cv : 0;
+        rc = chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total, first, end, Cv)
                      : verify_whole(fv, rd, n_pieces, piece_length, total, first, end);
         if (!rc && !chunked) {
             while (fv.done < count && !rc) {

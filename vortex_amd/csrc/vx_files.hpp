@@ -214,6 +214,28 @@ class DirectIo {
     }
     uint64_t direct_bytes() const { return direct_bytes_.load(std::memory_order_relaxed); }
 
+    // Fraction of about `samples` pages, spread over the mapped files by size
+    // (mid-points of equal parts, at least one per file), that the page cache
+    // holds: mincore, no faults.  1 when nothing is mapped (O_DIRECT off, or
+    // no file it applies to), so the caller's warm choice stands.
+    double resident_fraction(uint64_t samples = 256) const {
+        uint64_t total = 0;
+        for (size_t f = 0; f < map_.size(); ++f)
+            if (map_[f]) total += size_[f];
+        if (total == 0 || samples == 0) return 1.0;
+        uint64_t hit = 0, seen = 0;
+        for (size_t f = 0; f < map_.size(); ++f) {
+            if (!map_[f]) continue;
+            const uint64_t pages = (size_[f] + kBlock - 1) / kBlock;
+            const uint64_t k = std::min<uint64_t>(pages, std::max<uint64_t>(1, samples * size_[f] / total));
+            for (uint64_t i = 0; i < k; ++i) {
+                hit += resident((uint32_t)f, (int64_t)(((2 * i + 1) * pages / (2 * k)) * kBlock)) ? 1 : 0;
+                ++seen;
+            }
+        }
+        return seen ? (double)hit / (double)seen : 1.0;
+    }
+
   private:
     bool resident(uint32_t f, int64_t off) const {
         unsigned char v = 0;
