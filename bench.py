@@ -453,7 +453,8 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3):
     def trace_of(pool):
         tr = pool.last_verify()
         keep = ("wall_ms", "read_busy_ms", "read_span_ms", "first_read_ms", "copy_busy_ms", "copy_span_ms", "tail_ms",
-                "read_GiBps", "read_GiBps_per_thread", "copy_GiBps", "copy_busy_frac", "rounds", "readers")
+                "read_GiBps", "read_GiBps_per_thread", "copy_GiBps", "copy_busy_frac", "rounds", "readers",
+                "direct_bytes", "chunk_bytes")
         return {k: (round(tr[k], 3) if isinstance(tr[k], float) else tr[k]) for k in keep}
 
     try:
