@@ -106,9 +106,11 @@ int vx_create(const vx_config* cfg, vx_ctx** out);
 int vx_destroy(vx_ctx* ctx);
 
 /* Pin and device-map a host range (e.g. a BufferPool's AnonymousMmap,
- * buf_ring.rs:24-42) so pieces inside it are pulled straight to the GPU (one
- * gather kernel per batch reads them over PCIe) instead of being staged
- * through an internal pinned copy.  Ranges must not overlap. */
+ * buf_ring.rs:24-42) so pieces inside it reach the GPU without an internal
+ * pinned copy: an async batch whose pieces are all registered and 16-byte
+ * aligned is hashed by a kernel that reads them over PCIe itself (zero-copy
+ * slots); host batches pull them with one gather kernel per round.  Ranges
+ * must not overlap. */
 int vx_register_host_buffer(vx_ctx* ctx, void* ptr, size_t len);
 int vx_unregister_host_buffer(vx_ctx* ctx, void* ptr);
 
