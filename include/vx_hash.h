@@ -272,6 +272,12 @@ typedef struct vx_plan {
 } vx_plan;
 int vx_plan_verify(uint64_t n_pieces, uint32_t piece_length, uint64_t total_length, uint32_t cpu_threads,
                    double cpu_thread_rate, vx_plan* out);
+/* The same plan for a verify split over n_gpus contexts, one per GPU
+ * (vx_verify_files_multi): gpu_transfer_s is each GPU's share over its own
+ * link; gpu_chain_s, one piece's chain, does not shrink with more GPUs.
+ * n_gpus 0 or 1 gives vx_plan_verify's answer. */
+int vx_plan_verify_gpus(uint64_t n_pieces, uint32_t piece_length, uint64_t total_length, uint32_t cpu_threads,
+                        double cpu_thread_rate, uint32_t n_gpus, vx_plan* out);
 
 /* ---- device-resident batches (the hot path; no context needed) --------
  * These entries validate what they can see on the host — NULL pointers, the

@@ -232,6 +232,40 @@ def _plan(n, pl, total, threads=16, rate=2.0e9):
     return rc, p
 
 
+def _plan_g(n, pl, total, threads, g, rate=2.2e9):
+    from vortex_amd import _lib
+
+    p = _lib.vx_plan()
+    assert _lib.lib().vx_plan_verify_gpus(n, pl, total, threads, rate, g, ctypes.byref(p)) == 0
+    return p
+
+
+def test_plan_verify_gpus_host(built):
+    """vx_plan_verify_gpus (include/vx_hash.h): the bytes split over n_gpus
+    links, one piece's chain unchanged.  n_gpus 0/1 is vx_plan_verify; on a
+    full node (128 threads) linux-mint's 2 MiB pieces stay on the CPU pool
+    whatever the GPU count (a 2 MiB chain is ~25 ms), while many short or
+    many long pieces go to 8 GPUs (INTEGRATION.md "A whole node")."""
+    MiB = 1 << 20
+    fields = ("gpu_s", "gpu_chain_s", "gpu_transfer_s", "cpu_s", "use_gpu")
+    for n, pl, total, t in ((1387, 2 * MiB, 2907832320, 16), (174, 16 * MiB, 174 * 16 * MiB, 16),
+                            (11093, 256 * 1024, 11093 * 256 * 1024, 64)):
+        _, base = _plan(n, pl, total, threads=t, rate=2.2e9)
+        for g in (0, 1):
+            q = _plan_g(n, pl, total, t, g)
+            assert all(getattr(q, f) == getattr(base, f) for f in fields), (n, g)
+        q8 = _plan_g(n, pl, total, t, 8)
+        assert abs(q8.gpu_transfer_s * 8 - base.gpu_transfer_s) < 1e-12 and q8.gpu_chain_s == base.gpu_chain_s
+        assert q8.gpu_s <= base.gpu_s and q8.cpu_s == base.cpu_s
+    for g in (1, 2, 4, 8):  # full node, linux-mint: chain-bound against a 128-thread pool
+        q = _plan_g(1387, 2 * MiB, 2907832320, 128, g)
+        assert q.use_gpu == 0 and q.gpu_s > q.gpu_chain_s > q.cpu_s
+    assert _plan_g(11093, 256 * 1024, 11093 * 256 * 1024, 64, 1).use_gpu == 0   # PCIe-bound on one link
+    assert _plan_g(11093, 256 * 1024, 11093 * 256 * 1024, 64, 8).use_gpu == 1   # eight links
+    assert _plan_g(8192, 16 * MiB, 8192 * 16 * MiB, 128, 1).use_gpu == 0
+    assert _plan_g(8192, 16 * MiB, 8192 * 16 * MiB, 128, 8).use_gpu == 1
+
+
 def test_plan_verify_host(built):
     """vx_plan_verify, host-only: the BASELINE re-verify
     geometry goes to the GPU, a few very long pieces stay on the caller's

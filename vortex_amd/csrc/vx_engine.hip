@@ -2146,6 +2146,16 @@ int vx_sha1_device_ragged_hint(const void* d_base, const uint64_t* d_offsets, co
 // caller's own pool is the safe choice.
 int vx_plan_verify(uint64_t n_pieces, uint32_t piece_length, uint64_t total_length, uint32_t cpu_threads,
                    double cpu_thread_rate, vx_plan* out) {
+    return vx_plan_verify_gpus(n_pieces, piece_length, total_length, cpu_threads, cpu_thread_rate, 1, out);
+}
+
+// The same model over n_gpus contexts (vx_verify_files_multi):
+// each GPU's share of the bytes crosses its own PCIe link, so the transfer
+// term divides by n_gpus; one piece's chain does not shrink, which is why a
+// host with many cores can keep its pool against any number of GPUs when the
+// pieces are long (INTEGRATION.md "A whole node is a different host").
+int vx_plan_verify_gpus(uint64_t n_pieces, uint32_t piece_length, uint64_t total_length, uint32_t cpu_threads,
+                        double cpu_thread_rate, uint32_t n_gpus, vx_plan* out) {
     if (!out || piece_length == 0) return fail(VX_EINVAL, "vx_plan_verify: bad argument");
     if (n_pieces != (total_length + piece_length - 1) / piece_length)
         return fail(VX_EINVAL, "vx_plan_verify: n_pieces does not match total_length");
@@ -2158,7 +2168,7 @@ int vx_plan_verify(uint64_t n_pieces, uint32_t piece_length, uint64_t total_leng
     *out = vx_plan{};
     if (n_pieces == 0) return 0;
     out->gpu_chain_s = blocks * kChainBlock;
-    out->gpu_transfer_s = (double)total_length / kPcieRate;
+    out->gpu_transfer_s = (double)total_length / kPcieRate / std::max<uint32_t>(1, n_gpus);
     out->gpu_s = std::max(out->gpu_transfer_s, out->gpu_chain_s) + kSetup +
                  kOverlapLoss * std::min(out->gpu_transfer_s, out->gpu_chain_s);
     out->cpu_s = std::ceil((double)n_pieces / threads) * (L / rate);
