@@ -171,15 +171,34 @@ def test_verify_files_cold_direct_reads(built, gpu, tmp_path, monkeypatch, pl, c
     the filesystem takes O_DIRECT.  With VX_VERIFY_COLD_CHUNK (off by
     default) evicted calls of pieces >= 2 MiB run 1 MiB rounds (many windows
     of the 16 MiB slots); cached ones, and every call by default, 256 KiB."""
+    import pathlib
+    import shutil
+    import tempfile
+
+    def takes_direct(d):
+        try:
+            fd = os.open(os.path.join(d, "probe"), os.O_CREAT | os.O_RDWR | os.O_DIRECT, 0o600)
+            os.close(fd)
+            return True
+        except OSError:
+            return False
+
+    # a disk-backed directory when pytest's tmp_path is tmpfs (no O_DIRECT there)
+    where, own = tmp_path, None
+    if not takes_direct(str(tmp_path)) and os.path.isdir("/var/tmp") and os.access("/var/tmp", os.W_OK):
+        own = tempfile.mkdtemp(prefix="vx_cold_", dir="/var/tmp")
+        where = pathlib.Path(own)
+    direct_ok = takes_direct(str(where))
+    try:
+        _cold_direct_reads(where, pl, cold_chunk, direct_ok, monkeypatch)
+    finally:
+        if own:
+            shutil.rmtree(own, ignore_errors=True)
+
+
+def _cold_direct_reads(tmp_path, pl, cold_chunk, direct_ok, monkeypatch):
     from vortex_amd.hash_pool import HashPool
 
-    d = str(tmp_path)
-    try:
-        fd = os.open(os.path.join(d, "probe"), os.O_CREAT | os.O_RDWR | os.O_DIRECT, 0o600)
-        os.close(fd)
-        direct_ok = True
-    except OSError:
-        direct_ok = False
     sizes = [3 * pl + 4096 * 3, 5 * pl, 2 * pl + 777, pl + 1, 9 * pl]  # aligned and misaligned file starts
     paths, exp = _torrent(tmp_path, pl, sizes, 31)
     with open(paths[1], "r+b") as f:  # one flipped byte in an aligned region
