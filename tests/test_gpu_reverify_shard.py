@@ -189,6 +189,7 @@ def test_verify_files_cold_direct_reads(built, gpu, tmp_path, monkeypatch, pl, c
         own = tempfile.mkdtemp(prefix="vx_cold_", dir="/var/tmp")
         where = pathlib.Path(own)
     direct_ok = takes_direct(str(where))
+    print(f"cold re-verify test dir {where}: O_DIRECT {'yes' if direct_ok else 'no'}")
     try:
         _cold_direct_reads(where, pl, cold_chunk, direct_ok, monkeypatch)
     finally:
