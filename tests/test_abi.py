@@ -264,6 +264,10 @@ def test_plan_verify_gpus_host(built):
     assert _plan_g(11093, 256 * 1024, 11093 * 256 * 1024, 64, 8).use_gpu == 1   # eight links
     assert _plan_g(8192, 16 * MiB, 8192 * 16 * MiB, 128, 1).use_gpu == 0
     assert _plan_g(8192, 16 * MiB, 8192 * 16 * MiB, 128, 8).use_gpu == 1
+    from vortex_amd.hash_pool import plan_verify  # the Python mirror
+    d = plan_verify(1387, 2 * MiB, 2907832320)
+    assert d["use_gpu"] is True and d["gpu_s"] < d["cpu_s"]
+    assert plan_verify(1387, 2 * MiB, 2907832320, cpu_threads=128, cpu_thread_rate=2.2e9, n_gpus=8)["use_gpu"] is False
 
 
 def test_plan_verify_host(built):

@@ -357,3 +357,17 @@ def piece_len(index: int, num_pieces: int, piece_length: int, total_length: int)
 
 
 __all__ = ["DownloadedPiece", "HashPool", "verify_pieces", "verify_files_multi", "piece_len"]
+
+
+def plan_verify(n_pieces: int, piece_length: int, total_length: int, cpu_threads: int = 0,
+                cpu_thread_rate: float = 0.0, n_gpus: int = 1) -> dict:
+    """Where a bulk verify should run (include/vx_hash.h vx_plan_verify_gpus,
+    host-only, no GPU): the predicted seconds of the GPU path over n_gpus
+    contexts and of the caller's pool of cpu_threads (torrent.rs:724-740), and
+    use_gpu.  0 threads / rate = 16 threads at 2.2e9 B/s (SHA-NI)."""
+    p = _lib.vx_plan()
+    check(lib().vx_plan_verify_gpus(n_pieces, piece_length, total_length, cpu_threads, cpu_thread_rate, n_gpus,
+                                    ctypes.byref(p)), "vx_plan_verify_gpus")
+    out = {name: getattr(p, name) for name, _ in _lib.vx_plan._fields_ if not name.startswith("_")}
+    out["use_gpu"] = bool(out["use_gpu"])
+    return out
