@@ -520,7 +520,7 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3):
     return warm, cold
 
 
-def roofline(n: int, plen: int, kern_ms: float, achieved: float, workload: str) -> dict:
+def roofline(n: int, plen: int, kern_ms: float, achieved: float, workload: str, clock: dict | None = None) -> dict:
     """Roofline record of the dominant kernel (sha1_uniform_kernel).
 
     achieved/peak/frac: algorithmic bytes per launch / HIP-event launch time
@@ -572,6 +572,16 @@ def roofline(n: int, plen: int, kern_ms: float, achieved: float, workload: str) 
                    "source": ent.get("source")}
     except (OSError, ValueError):
         pass
+    clock_run = None
+    if clock and clock.get("GHz_mean"):
+        f_run = clock["GHz_mean"] * 1e9
+        ceil_run = simds * 64 / 4.0 * f_run
+        clock_run = dict(clock, one_wave_issue_at_run_clock={
+            "peak_Tops": round(ceil_run / 1e12, 2), "frac": round(ops / ceil_run, 4),
+            "note": "the one-wave VOP3 issue ceiling (4 cycles per op per SIMD) at the shader clock measured "
+                    "over this run's timed steps; frac near 1 = issue-bound at the clock the chip held"})
+    elif clock:
+        clock_run = clock
     return {"bound": "valu", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK, 4), "traffic": traffic,
             "traffic_ratio": round(traffic / (n * plen), 5) if traffic else None,
@@ -603,10 +613,77 @@ def roofline(n: int, plen: int, kern_ms: float, achieved: float, workload: str) 
                                    "at (or above) the slow state's clock and is at that clock's ceiling"},
                      "simd32_vop2_only": {"peak_Tops": round(peak(2.0) / 1e12, 2), "frac": round(ops / peak(2.0), 4)},
                      "pmc": pmc,
+                     "clock_run": clock_run,
                      "note": "65,536 pieces = exactly one wave per SIMD. Every SHA-1 op but the schedule's "
                              "2-input xor and the feed-forward add is VOP3-only on gfx950, and a VOP3 op holds "
                              "its SIMD ~4.1 cycles however many waves share it, so 2 waves/SIMD (131,072 x "
                              "128 KiB) run no faster (DESIGN.md §4)"}}
+
+
+CLOCK_BLOCKS = 256  # stamp workgroups: 32 per XCC under round-robin dispatch
+
+
+def clock_from_stamps(before, after, khz: int) -> dict:
+    """Mean shader clock per XCC over the stretch two vx_tuning_clock_stamp
+    launches bracket (vortex_amd/csrc/vx_clock.hip).  before/after: [blocks,
+    3] int arrays of (shader cycles, real-time ticks, XCC id).  Each XCC's
+    counters are compared only with its own (the counters of different XCCs
+    need not agree), from the mean of its workgroups' stamps on each side."""
+    import numpy as np
+
+    b = np.asarray(before, dtype=np.float64).reshape(-1, 3)
+    a = np.asarray(after, dtype=np.float64).reshape(-1, 3)
+    per = {}
+    for x in sorted(set(int(v) for v in b[:, 2]) & set(int(v) for v in a[:, 2])):
+        bb, aa = b[b[:, 2] == x], a[a[:, 2] == x]
+        d_rt = aa[:, 1].mean() - bb[:, 1].mean()
+        d_cy = aa[:, 0].mean() - bb[:, 0].mean()
+        if d_rt > 0:
+            per[x] = d_cy / d_rt * khz * 1e3 / 1e9
+    span_ms = (a[:, 1].max() - b[:, 1].min()) / (khz * 1e3) * 1e3 if len(a) and len(b) else None
+    ghz = list(per.values())
+    return {"GHz_mean": round(float(np.mean(ghz)), 4) if ghz else None,
+            "GHz_per_xcc": {str(k): round(v, 4) for k, v in per.items()},
+            "GHz_min": round(min(ghz), 4) if ghz else None, "GHz_max": round(max(ghz), 4) if ghz else None,
+            "span_ms": round(span_ms, 3) if span_ms is not None else None, "wall_clock_kHz": khz,
+            "source": "s_memtime / s_memrealtime stamps of each XCC before and after the timed steps "
+                      "(vx_tuning_clock_stamp, vortex_amd/csrc/vx_clock.hip), same stream"}
+
+
+class ClockStamps:
+    """Two stamp launches on `stream` bracketing the timed steps."""
+
+    def __init__(self, dev, stream):
+        import torch
+
+        from vortex_amd._lib import lib
+
+        self.stream, self.dev = stream, dev
+        self.buf = [torch.zeros(3 * CLOCK_BLOCKS, dtype=torch.int64, device=dev) for _ in range(2)]
+        self.khz = lib().vx_tuning_wall_clock_khz(dev.index or 0)
+
+    def stamp(self, k: int) -> None:
+        from vortex_amd._lib import check, lib
+
+        check(lib().vx_tuning_clock_stamp(self.buf[k].data_ptr(), CLOCK_BLOCKS, self.stream.cuda_stream),
+              "vx_tuning_clock_stamp")
+
+    def result(self) -> dict:
+        if self.khz <= 0:
+            return {"error": f"wall clock rate unavailable ({self.khz})"}
+        return clock_from_stamps(self.buf[0].cpu().numpy(), self.buf[1].cpu().numpy(), self.khz)
+
+
+def device_identity(local: int) -> dict:
+    """Which physical GPU this rank hashed on (PCI bus id, UUID)."""
+    from vortex_amd._lib import check, lib
+
+    bus = ctypes.create_string_buffer(64)
+    uuid = ctypes.create_string_buffer(16)
+    check(lib().vx_tuning_device_identity(local, bus, 64, uuid), "vx_tuning_device_identity")
+    return {"device_index": local, "pci_bus_id": bus.value.decode().lower(), "uuid": uuid.raw.hex(),
+            "visible_devices": {k: os.environ[k] for k in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES",
+                                                          "CUDA_VISIBLE_DEVICES") if k in os.environ}}
 
 
 def _free_port() -> int:
@@ -626,17 +703,27 @@ def launch_cmd(args, argv, port: int) -> list:
 
 def launch_ranks(args, argv) -> int:
     """Start args.gpus ranks as a child process group and relay rank 0's JSON
-    line and the exit code.  Runs before anything touches the GPU (counting
-    devices does not initialise it on this ROCm build), and never execs."""
+    line and the exit code.  The parent never touches the GPU: it counts
+    devices from the KFD topology in sysfs (vortex_amd/topology.py — no HIP,
+    no torch), refuses when that count is below --gpus or unreadable, checks
+    that no HIP runtime is mapped in it before starting the launcher, and
+    never execs."""
     import subprocess
 
-    if not args.same_device:
-        import torch
+    from vortex_amd import topology
 
-        ndev = torch.cuda.device_count()
+    if not args.same_device:
+        ndev = topology.visible_gpus()
+        if ndev is None:
+            log(f"error: --gpus {args.gpus} but the KFD topology ({topology.KFD_NODES}) is unreadable; "
+                "refusing to guess the GPU count")
+            return 2
         if ndev < args.gpus:
             log(f"error: --gpus {args.gpus} but only {ndev} GPU(s) visible; refusing to report a smaller run")
             return 2
+    if topology.hip_runtime_mapped():
+        log("error: the launching process has the HIP runtime mapped; it must not touch the GPU")
+        return 3
     cmd = launch_cmd(args, argv, _free_port())
     log("launching", args.gpus, "ranks:", " ".join(cmd))
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
@@ -755,23 +842,28 @@ def main() -> int:
     torch.cuda.synchronize()
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    clk = ClockStamps(dev, stream)
+    ident = device_identity(local)
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     verdicts = None
+    clk.stamp(0)  # two 256-workgroup stamp launches bracket the steps (~10 us each)
     for k in range(args.steps):
         evs[k][0].record(stream)
         step()
         evs[k][1].record(stream)
         if distributed:
             verdicts = gather_verdicts(matched, n_total)
+    clk.stamp(1)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if distributed:
         dist.barrier()
     elapsed = t1 - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in evs) / args.steps
+    clock = clk.result()
     ranks = None
     if distributed:
         # The verdict all-gather alone, after the timed region: what the one
@@ -784,15 +876,26 @@ def main() -> int:
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - g0) / args.steps * 1e3
         # every rank's figures (max over ranks is what `value` uses)
-        mine = torch.tensor([elapsed, kern_ms, gather_ms], dtype=torch.float64,
+        mine = torch.tensor([elapsed, kern_ms, gather_ms, clock.get("GHz_mean") or 0.0], dtype=torch.float64,
                             device=dev if args.dist_backend == "nccl" else "cpu")
-        allr = torch.empty(3 * world, dtype=torch.float64, device=mine.device)
+        allr = torch.empty(4 * world, dtype=torch.float64, device=mine.device)
         dist.all_gather_into_tensor(allr, mine)
-        per = allr.view(world, 3).cpu().tolist()
+        per = allr.view(world, 4).cpu().tolist()
         elapsed, kern_ms = max(r[0] for r in per), max(r[1] for r in per)
+        # which physical GPU every rank ran on, and the world RCCL reported
+        idents = [None] * world
+        dist.all_gather_object(idents, dict(ident, rank=rank, world_size=dist.get_world_size()))
+        buses = [d["pci_bus_id"] for d in idents]
+        distinct = len(set(buses)) == world
+        if not args.same_device and not distinct:  # every rank sees the same list: all fail together
+            log(f"error: ranks share a GPU (bus ids {buses}); a {world}-GPU line needs {world} distinct devices")
+            dist.destroy_process_group()
+            return 4
         ranks = {"step_ms": [round(r[0] / args.steps * 1e3, 4) for r in per],
                  "kernel_ms": [round(r[1], 4) for r in per],
-                 "verdict_gather_ms": [round(r[2], 4) for r in per]}
+                 "verdict_gather_ms": [round(r[2], 4) for r in per],
+                 "clock_GHz": [round(r[3], 4) for r in per],
+                 "devices": idents, "distinct_devices": distinct}
 
     # Verdicts: exactly the corrupted pieces mismatch (checked on the gathered
     # table when N > 1, else locally).
@@ -825,7 +928,8 @@ def main() -> int:
                                + (f", {backend} all-gather of verdicts" if distributed else ""),
                    "pieces_per_gpu": n, "piece_len": plen, "total_GiB": round(total_bytes / GiB, 2),
                    "parallelism": f"piece-index shard x{world}"},
-        "roofline": roofline(n, plen, kern_ms, achieved, workload),
+        "roofline": roofline(n, plen, kern_ms, achieved, workload, clock),
+        "device": ident,
     }
     if ranks is not None:
         res["ranks"] = ranks

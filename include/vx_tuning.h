@@ -88,6 +88,17 @@ int vx_tuning_last_verify(const struct vx_ctx* ctx, vx_verify_trace* out);
 int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
                                    const void* d_expected, void* d_matched, void* stream, int variant);
 
+/* Shader-clock stamps (bench.py; vx_clock.hip): enqueue `blocks` one-wave
+ * workgroups on `stream`; workgroup b writes d_out[3b..3b+2] = (shader cycle
+ * counter, 100 MHz real-time counter, XCC id).  Two stamps bracketing a
+ * stretch of work on one stream give each XCC's mean shader clock over it. */
+int vx_tuning_clock_stamp(void* d_out, uint32_t blocks, void* stream);
+/* The real-time counter's rate in kHz (hipDeviceAttributeWallClockRate). */
+int vx_tuning_wall_clock_khz(int device);
+/* Physical identity of HIP device `device`: its PCI bus id ("dddd:bb:dd.f",
+ * NUL-terminated in bus_id[0..len), len >= 16) and 16-byte UUID. */
+int vx_tuning_device_identity(int device, char* bus_id, size_t len, char* uuid16);
+
 #ifdef __cplusplus
 }
 #endif

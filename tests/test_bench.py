@@ -55,17 +55,82 @@ def test_launch_command_shape():
 
 
 def test_plain_multi_gpu_run_without_gpus_fails_loudly():
-    import torch
+    """No KFD topology here (or fewer GPUs than asked): refuse before launching."""
+    from vortex_amd import topology
 
-    if torch.cuda.device_count() >= 2:
+    n = topology.visible_gpus()
+    if n is not None and n >= 2:
         pytest.skip("GPUs visible")
-    r = _run(["--gpus", "2"] + SMALL, timeout=120)  # counts devices, refuses before launching
+    r = _run(["--gpus", "2"] + SMALL, timeout=120)  # counts devices from sysfs, refuses before launching
     assert r.returncode == 2 and not _lines(r.stdout)
-    assert "GPU(s) visible" in r.stderr
-    if torch.cuda.device_count() == 0:
+    assert "refusing" in r.stderr
+    if not n:
         # rehearsal form: both ranks would share cuda:0; with no GPU the ranks die and so does the run
         r = _run(["--gpus", "2", "--same-device", "--dist-backend", "gloo"] + SMALL, timeout=240)
         assert r.returncode != 0 and not _lines(r.stdout)
+
+
+def _fake_kfd(tmp_path, nodes, renders):
+    """A KFD topology tree: nodes = [(gfx_target_version, drm_render_minor) or None (no properties)]."""
+    kfd = tmp_path / "nodes"
+    dri = tmp_path / "dri"
+    dri.mkdir()
+    for k, nd in enumerate(nodes):
+        d = kfd / str(k)
+        d.mkdir(parents=True)
+        if nd is not None:
+            gfx, minor = nd
+            (d / "properties").write_text(f"cpu_cores_count 0\nsimd_count 1024\ngfx_target_version {gfx}\n"
+                                          f"drm_render_minor {minor}\nlocation_id {4096 * k}\n")
+    for m in renders:
+        (dri / f"renderD{m}").write_text("")
+    return str(kfd), str(dri)
+
+
+def test_topology_count_from_sysfs(tmp_path):
+    """vortex_amd.topology counts GPU nodes (gfx_target_version != 0) whose
+    render node exists here and whose properties are readable, capped by every
+    *_VISIBLE_DEVICES variable that is set; CPU nodes never count."""
+    from vortex_amd import topology
+
+    # node 0: CPU; 1-4: GPUs, of which render 131 is not in this container; 5: properties hidden (cgroup)
+    kfd, dri = _fake_kfd(tmp_path, [(0, 0), (90500, 128), (90500, 129), (90500, 130), (90500, 131), None],
+                         [128, 129, 130])
+    assert topology.visible_gpus(kfd, dri, environ={}) == 3
+    assert [g["drm_render_minor"] for g in topology.kfd_gpus(kfd, dri)] == [128, 129, 130]
+    assert topology.visible_gpus(kfd, dri, environ={"HIP_VISIBLE_DEVICES": "0,1"}) == 2
+    assert topology.visible_gpus(kfd, dri, environ={"ROCR_VISIBLE_DEVICES": "1", "HIP_VISIBLE_DEVICES": "0,1"}) == 1
+    assert topology.visible_gpus(kfd, dri, environ={"CUDA_VISIBLE_DEVICES": ""}) == 0
+    assert topology.visible_gpus(str(tmp_path / "absent"), dri, environ={}) is None
+
+
+def test_launcher_parent_never_maps_hip():
+    """The parent's whole pre-launch path (sysfs count, refusal) runs without
+    the HIP runtime in the process (the same check launch_ranks makes before
+    it starts the launcher)."""
+    code = ("import sys; sys.argv = ['bench.py', '--gpus', '64'] + %r; import bench; rc = bench.main(); "
+            "from vortex_amd import topology; print('MAPPED' if topology.hip_runtime_mapped() else 'CLEAN', rc)"
+            % SMALL)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, cwd=ROOT,
+                       env={k: v for k, v in os.environ.items() if k != "WORLD_SIZE"})
+    assert r.stdout.split() == ["CLEAN", "2"], (r.stdout, r.stderr[-2000:])
+
+
+@pytest.mark.gpu
+def test_plain_multi_gpu_refused_on_one_gpu_box(built, gpu):
+    """On the 1-GPU box a plain `bench.py --gpus 2` (no --same-device) must be
+    refused from the sysfs count — rc 2, no result line — by a parent that
+    never mapped the HIP runtime, and the sysfs count must equal what HIP sees
+    (torch, in this test process)."""
+    import torch
+
+    from vortex_amd import topology
+
+    assert topology.visible_gpus() == torch.cuda.device_count() == 1
+    r = _run(["--gpus", "2"] + SMALL, timeout=120)
+    assert r.returncode == 2 and not _lines(r.stdout), r.stderr[-2000:]
+    assert "only 1 GPU(s) visible" in r.stderr
+    test_launcher_parent_never_maps_hip()
 
 
 @pytest.mark.gpu
@@ -83,6 +148,11 @@ def test_plain_bench_launches_its_ranks(built, gpu, n):
     rk = res["ranks"]  # every rank's step, kernel and verdict-gather times
     assert all(len(rk[k]) == n for k in ("step_ms", "kernel_ms", "verdict_gather_ms"))
     assert max(rk["step_ms"]) == pytest.approx(res["ms_per_step"], rel=1e-3)
+    # identity: every rank names its device; all share the one GPU here, and the line says so
+    assert [d["rank"] for d in rk["devices"]] == list(range(n))
+    assert all(d["world_size"] == n and d["pci_bus_id"] == rk["devices"][0]["pci_bus_id"] for d in rk["devices"])
+    assert rk["distinct_devices"] is False
+    assert all(1.0 < g < 3.0 for g in rk["clock_GHz"])
 
 
 @pytest.mark.gpu
@@ -99,3 +169,25 @@ def test_bench_rccl_world_size_1(built, gpu):
     assert res["n_gpus"] == 1 and res["world_size"] == 1 and res["backend"] == "nccl"
     assert "nccl all-gather of verdicts" in res["config"]["workload"]
     assert len(res["ranks"]["verdict_gather_ms"]) == 1 and res["ranks"]["verdict_gather_ms"][0] > 0
+    assert res["ranks"]["distinct_devices"] is True and res["ranks"]["devices"][0]["world_size"] == 1
+    clk = res["roofline"]["valu"]["clock_run"]
+    assert 1.0 < clk["GHz_mean"] < 3.0 and clk["one_wave_issue_at_run_clock"]["frac"] > 0
+
+
+def test_clock_from_stamps():
+    """Per-XCC clock = shader cycles / real-time ticks x the tick rate, each XCC
+    against its own counters (their offsets differ)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    before, after = [], []
+    for b in range(16):
+        x = b % 8
+        off = 10 ** 12 * x  # XCCs' cycle counters disagree by a constant
+        ghz = 2.0 + 0.05 * x
+        before.append((off + 1000, 5_000, x))
+        after.append((off + 1000 + int(ghz * 1e9 * 0.1), 5_000 + 10_000_000, x))  # 0.1 s at 100 MHz
+    r = bench.clock_from_stamps(before, after, 100_000)
+    assert r["GHz_per_xcc"]["0"] == pytest.approx(2.0, rel=1e-6)
+    assert r["GHz_per_xcc"]["7"] == pytest.approx(2.35, rel=1e-6)
+    assert r["GHz_mean"] == pytest.approx(2.175, rel=1e-4) and r["span_ms"] == pytest.approx(100.0)

@@ -39,7 +39,8 @@ EXPORTS = (
     "vx_synth_fill", "vx_sha1_device_uniform_variant", "vx_sha1_device_ragged_variant",
     "vx_tuning_chunk_rounds", "vx_tuning_gather_tiles", "vx_tuning_zero_copy_slots", "vx_tuning_zero_copy_plan", "vx_tuning_zero_copy_kernel", "vx_tuning_plan_ragged", "vx_tuning_chunk_schedule",
     "vx_tuning_fail_submit_after", "vx_plan_verify", "vx_plan_verify_gpus", "vx_get_stats", "vx_reset_stats",
-    "vx_tuning_fail_launch_after", "vx_tuning_last_verify",
+    "vx_tuning_fail_launch_after", "vx_tuning_last_verify", "vx_tuning_clock_stamp", "vx_tuning_wall_clock_khz",
+    "vx_tuning_device_identity",
 )
 
 
@@ -134,6 +135,9 @@ def _declare(L: ctypes.CDLL) -> None:
         "vx_tuning_fail_submit_after": ([vp, c.c_int64], None),
         "vx_tuning_fail_launch_after": ([vp, c.c_int64], None),
         "vx_tuning_last_verify": ([vp, c.POINTER(vx_verify_trace)], c.c_int),
+        "vx_tuning_clock_stamp": ([vp, c.c_uint32, vp], c.c_int),
+        "vx_tuning_wall_clock_khz": ([c.c_int], c.c_int),
+        "vx_tuning_device_identity": ([c.c_int, c.c_char_p, c.c_size_t, c.c_char_p], c.c_int),
         "vx_plan_verify": ([c.c_uint64, c.c_uint32, c.c_uint64, c.c_uint32, c.c_double, c.POINTER(vx_plan)], c.c_int),
         "vx_plan_verify_gpus": ([c.c_uint64, c.c_uint32, c.c_uint64, c.c_uint32, c.c_double, c.c_uint32,
                                  c.POINTER(vx_plan)], c.c_int),
