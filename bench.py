@@ -441,13 +441,10 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3):
     import oracle
     from vortex_amd.hash_pool import HashPool
 
-    pl, total = 2097152, 2907832320
-    n = (total + pl - 1) // pl
-    last = total - (n - 1) * pl
+    pl = 2097152
     threads = cpu_share()
     d = reverify_dir()
     path = os.path.join(d, f"vx_bench_linuxmint_{os.getpid()}.iso")
-    buf = ctypes.create_string_buffer(pl)
     t0 = time.perf_counter()
 
     def trace_of(pool):
@@ -458,13 +455,7 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3):
         return {k: (round(tr[k], 3) if isinstance(tr[k], float) else tr[k]) for k in keep}
 
     try:
-        with open(path, "wb") as f:
-            for i in range(n):
-                L = last if i == n - 1 else pl
-                oracle.lib().vxo_gen_piece(0x5EED0005, i, L, 0, buf)
-                f.write(memoryview(buf)[:L])
-            f.flush()
-            os.fsync(f.fileno())  # writeback done before anything is timed
+        total, n, last = write_linuxmint_file(path)
         t_write = time.perf_counter() - t0
         exp = oracle.pool_digest_synth(0x5EED0005, 0, n, pl, last_index=n - 1, last_len=last, threads=threads)
         legs = {}
@@ -518,6 +509,136 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3):
                  "sample": f"the same file with fsync + POSIX_FADV_DONTNEED before every call (reads from "
                            f"{where['fs']}), GPU and CPU pool alternating, median of {cold_reps}"})
     return warm, cold
+
+
+def write_linuxmint_file(path: str, scale: float = 1.0):
+    """The config-5 torrent's data (linux-mint geometry: 2 MiB pieces, last
+    piece 1,179,648 B; `scale` < 1 keeps the piece length and shrinks the
+    piece count, for rehearsals), synthetic, fsync'd.  Returns (total, n, last)."""
+    import oracle  # the checker: generates the bytes and, below, the expected table
+
+    pl, total = 2097152, 2907832320
+    if scale < 1.0:
+        total = max(2, int((total // pl) * scale)) * pl + 1179648
+    n = (total + pl - 1) // pl
+    last = total - (n - 1) * pl
+    buf = ctypes.create_string_buffer(pl)
+    with open(path, "wb") as f:
+        for i in range(n):
+            L = last if i == n - 1 else pl
+            oracle.lib().vxo_gen_piece(0x5EED0005, i, L, 0, buf)
+            f.write(memoryview(buf)[:L])
+        f.flush()
+        os.fsync(f.fileno())  # writeback done before anything is timed
+    return total, n, last
+
+
+def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, same_device: bool, scale: float = 1.0,
+                       reps: int = 3, cold_reps: int = 2) -> dict | None:
+    """BASELINE config 5 across the N GPUs of the node: rank 0
+    writes the linux-mint-geometry file; every rank re-verifies its contiguous
+    piece range (shard.shard_range, vx_verify_files_range) on its own GPU,
+    reading its bytes over its own PCIe link, warm (page cache) and cold
+    (rank 0 evicts the file before each call: fsync + POSIX_FADV_DONTNEED).
+    A call's time is the slowest rank's; every verdict is gathered and checked
+    on rank 0.  Beside it, rank 0 times the CPU restatement of vortex's
+    re-verify (oracle/pool_oracle.cpp, the par_iter of torrent.rs:724-740)
+    with every CPU of the node, while the GPU ranks wait.  Returns the record
+    on rank 0, None elsewhere."""
+    import torch
+    import torch.distributed as dist
+
+    import oracle
+    from vortex_amd import shard
+    from vortex_amd.hash_pool import HashPool
+
+    node_cpus = len(os.sched_getaffinity(0))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    io_threads = max(2, min(16, node_cpus // max(1, local_world)))
+    obj = [None]
+    if rank == 0:
+        d = reverify_dir()
+        path = os.path.join(d, f"vx_bench_multi_linuxmint_{os.getpid()}.iso")
+        t0 = time.perf_counter()
+        total, n, last = write_linuxmint_file(path, scale)
+        exp = oracle.pool_digest_synth(0x5EED0005, 0, n, 2097152, last_index=n - 1, last_len=last,
+                                       threads=min(node_cpus, 64))
+        obj = [{"path": path, "dir": d, "total": total, "n": n, "exp": exp, "write_s": time.perf_counter() - t0}]
+    dist.broadcast_object_list(obj, src=0)
+    spec = obj[0]
+    path, total, n, exp = spec["path"], spec["total"], spec["n"], spec["exp"]
+    pl = 2097152
+    first, count = shard.shard_range(n, world, rank)
+    vdev = torch.device("cpu") if backend == "gloo" else dev
+    legs = {"warm": [], "cold": []}
+    traces = {"warm": [], "cold": []}
+    cpu = {"warm": [], "cold": []}
+    def agree(flag: bool) -> bool:  # every rank takes the same branch, so no rank waits alone
+        flags = [None] * world
+        dist.all_gather_object(flags, bool(flag))
+        return all(flags)
+
+    cpu_ok = True
+    try:
+        with HashPool(pl, device=local, slots=4, slot_bytes=512 << 20, batch_pieces=4096) as pool:
+            got, bad = pool.verify_files([path], [total], pl, exp, io_threads=io_threads, first=first, count=count)
+            if not agree(all(got) and bad == 0):
+                raise RuntimeError("multi-GPU re-verify: a rank's warm-up verdicts differ from the expected table")
+            for leg, k in (("warm", reps), ("cold", cold_reps)):
+                for _ in range(k):
+                    if leg == "cold" and rank == 0:
+                        drop_cache(path)
+                    dist.barrier()
+                    t0 = time.perf_counter()
+                    got, bad = pool.verify_files([path], [total], pl, exp, io_threads=io_threads, first=first,
+                                                 count=count)
+                    el = time.perf_counter() - t0
+                    tr = pool.last_verify()
+                    verdicts = shard.gather_verdicts(torch.tensor(got, dtype=torch.uint8, device=vdev), n)
+                    times = [None] * world
+                    dist.all_gather_object(times, {"s": el, "bad": bad, "read_GiBps": tr["read_GiBps"],
+                                                   "copy_busy_frac": tr["copy_busy_frac"],
+                                                   "direct_bytes": tr["direct_bytes"]})
+                    if int(verdicts.sum()) != n or any(t["bad"] for t in times):  # the same on every rank
+                        raise RuntimeError("multi-GPU re-verify: verdicts differ from the expected table")
+                    if rank == 0:
+                        legs[leg].append(max(t["s"] for t in times))
+                        traces[leg].append([{k2: (round(v, 3) if isinstance(v, float) else v) for k2, v in t.items()}
+                                            for t in times])
+                    # the CPU pool on the whole node, GPU ranks idle at the barrier
+                    if rank == 0:
+                        if leg == "cold":
+                            drop_cache(path)
+                        t0 = time.perf_counter()
+                        ok = oracle.pool_verify_files([path], [total], pl, exp, threads=node_cpus)
+                        cpu[leg].append(time.perf_counter() - t0)
+                        cpu_ok = cpu_ok and all(ok)
+                    dist.barrier()
+    finally:
+        dist.barrier()
+        if rank == 0 and os.path.exists(path):
+            os.unlink(path)
+    if rank != 0:
+        return None
+
+    def med(v):
+        return sorted(v)[len(v) // 2]
+
+    out = {}
+    for leg in ("warm", "cold"):
+        g, c = med(legs[leg]), med(cpu[leg])
+        out[leg] = {"value": round(total / g / GiB, 2), "unit": "GiB/s", "s_runs": [round(t, 4) for t in legs[leg]],
+                    "cpu_pool": {"value": round(total / c / GiB, 2), "unit": "GiB/s", "cores": node_cpus,
+                                 "kind": "port", "s_runs": [round(t, 4) for t in cpu[leg]]},
+                    "gpu_over_cpu": round(c / g, 3), "rank_traces": traces[leg]}
+    out.update({"ranks": world, "same_device": same_device, "io_threads_per_rank": io_threads,
+                "pieces": n, "bytes": total, "write_s": round(spec["write_s"], 2), "cpu_pool_verdicts_ok": cpu_ok,
+                "file": {"dir": spec["dir"], "fs": fs_type(spec["dir"])},
+                "sample": f"config 5 split over {world} ranks by piece index (vx_verify_files_range per rank, own "
+                          f"GPU and PCIe link): {n} x 2 MiB pieces ({total} B, linux-mint geometry, synthetic), "
+                          f"warm median of {reps}, cold (evicted) median of {cold_reps}; the slowest rank's time; "
+                          f"CPU pool restatement with all {node_cpus} node CPUs beside it"})
+    return out
 
 
 def roofline(n: int, plen: int, kern_ms: float, achieved: float, workload: str, clock: dict | None = None) -> dict:
@@ -767,7 +888,9 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-ragged", action="store_true", help="skip the config-3 leg")
-    ap.add_argument("--no-reverify", action="store_true", help="skip the config-5 leg")
+    ap.add_argument("--no-reverify", action="store_true", help="skip the config-5 legs (N=1 and N>1)")
+    ap.add_argument("--reverify-multi-scale", type=float, default=1.0,
+                    help="N>1 re-verify leg: fraction of linux-mint's pieces (rehearsals)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm, the real path) or gloo (single-GPU multi-rank rehearsal)")
     ap.add_argument("--same-device", action="store_true",
@@ -933,6 +1056,21 @@ def main() -> int:
     }
     if ranks is not None:
         res["ranks"] = ranks
+    if distributed and world > 1 and not args.no_reverify:
+        # config 5 across the node's GPUs: the one configuration where
+        # several PCIe links can beat the node's own CPU pool; every rank takes part
+        del data, matched, expected
+        torch.cuda.empty_cache()
+        try:
+            rm = reverify_multi_leg(rank, world, local, dev, backend, args.same_device, args.reverify_multi_scale)
+        except Exception as e:  # noqa: BLE001  (recorded in the line; the checks raise on every rank alike)
+            import traceback
+
+            traceback.print_exc()
+            rm = {"error": f"{type(e).__name__}: {e}"}
+        if rank == 0:
+            res["reverify_multi"] = rm
+            log("reverify_multi:", {k: rm[k].get("value") for k in ("warm", "cold")} if "warm" in rm else rm)
     if rank == 0 and world == 1:
         # Extra legs (N=1 only): the other BASELINE configs and
         # the host-resident path, each with its own correctness check.  A leg

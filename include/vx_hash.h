@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define VX_ABI_VERSION 1
+#define VX_ABI_VERSION 2
 
 /* Error codes (negative errno values). */
 #define VX_OK 0
@@ -77,12 +77,27 @@ typedef struct vx_completion {
     uint8_t _pad[3];
 } vx_completion;
 
+/* Everything a caller may choose is here; the engine reads no environment
+ * variables.  Start from vx_config_default() and change fields (ABI 2 added
+ * the six after slot_bytes; vx_create rejects values outside their ranges). */
 typedef struct vx_config {
-    int32_t device;          /* HIP device ordinal                                   */
-    uint32_t max_piece_len;  /* bytes; torrent piece_length (torrent.rs:344 pool size) */
-    uint32_t batch_pieces;   /* launch a batch once this many pieces are queued      */
-    uint32_t slots;          /* batches in flight (each has its own stream + arena)  */
-    uint64_t slot_bytes;     /* device arena bytes per slot (>= max_piece_len)       */
+    int32_t device;             /* HIP device ordinal                                   */
+    uint32_t max_piece_len;     /* bytes; torrent piece_length (torrent.rs:344 pool size) */
+    uint32_t batch_pieces;      /* launch a batch once this many pieces are queued      */
+    uint32_t slots;             /* batches in flight (each has its own stream + arena)  */
+    uint64_t slot_bytes;        /* device arena bytes per slot (>= max_piece_len)       */
+    uint32_t zero_copy;         /* 1 (default): a batch whose pieces are all registered and 16-byte aligned is
+                                 * hashed straight out of host memory; 0: such pieces are gathered into HBM first */
+    uint32_t direct_io;         /* re-verify: 1 (default) reads uncached, 4 KiB-aligned ranges with O_DIRECT;
+                                 * 0: every read through the page cache (vortex's own pread)                   */
+    uint32_t batch_chunk;       /* host batches of long pieces: bytes per resumable round (default 65536,
+                                 * multiple of 4096); 0: whole pieces per slot                                  */
+    uint32_t verify_chunk;      /* re-verify: bytes per resumable round (multiple of 4096); 0 (default): chosen
+                                 * per call, 256 KiB when one window holds every piece, else 128 KiB           */
+    uint32_t verify_cold_chunk; /* re-verify of data not in the page cache: bytes per round (multiple of 4096);
+                                 * 0 (default): as when cached                                                  */
+    uint32_t verify_ramp;       /* re-verify: first and last rounds shrink to chunk / 2^(d+1), d = 0..5
+                                 * (default 1; 0: no ramp)                                                      */
 } vx_config;
 
 typedef struct vx_ctx vx_ctx;
@@ -107,10 +122,11 @@ int vx_destroy(vx_ctx* ctx);
 
 /* Pin and device-map a host range (e.g. a BufferPool's AnonymousMmap,
  * buf_ring.rs:24-42) so pieces inside it reach the GPU without an internal
- * pinned copy: an async batch whose pieces are all registered and 16-byte
- * aligned is hashed by a kernel that reads them over PCIe itself (zero-copy
- * slots); host batches pull them with one gather kernel per round.  Ranges
- * must not overlap. */
+ * pinned copy: any batch slot whose pieces are all registered and 16-byte
+ * aligned — async, or a host batch of short pieces — is hashed by a kernel
+ * that reads them over PCIe itself (zero-copy slots, vx_config.zero_copy);
+ * host batches of long pieces pull them with one gather kernel per resumable
+ * round.  Ranges must not overlap. */
 int vx_register_host_buffer(vx_ctx* ctx, void* ptr, size_t len);
 int vx_unregister_host_buffer(vx_ctx* ctx, void* ptr);
 

@@ -32,20 +32,21 @@ uint64_t vx_tuning_gather_tiles(const struct vx_ctx* ctx);
  * and aligned, read from host memory by the hash kernel itself, no gather;
  * DESIGN.md §6.5). */
 uint64_t vx_tuning_zero_copy_slots(const struct vx_ctx* ctx);
-/* How the default policy (VX_ZERO_COPY unset, VX_ZC_LOADER=2) hashes a slot
- * of n registered, aligned pieces of total_len bytes: 1 the zero-copy pair,
- * 2 the zero-copy kernel with a loader wave (n < 128, a latency-bound batch);
- * 0 (gather + hash) is only taken with VX_ZERO_COPY=0.  Host-only
- * (DESIGN.md §6.5). */
+/* ... of them, the slots hashed in the three-wave form (a loader wave beside
+ * the pair; what the policy picks for slots of fewer than 128 pieces). */
+uint64_t vx_tuning_zero_copy_loader_slots(const struct vx_ctx* ctx);
+/* How a context with zero_copy = 1 hashes a slot of n registered, aligned
+ * pieces of total_len bytes: 1 the zero-copy pair, 2 the zero-copy kernel
+ * with a loader wave (n < 128, a latency-bound batch); 0 (gather + hash) is
+ * only taken with zero_copy = 0.  Host-only. */
 int vx_tuning_zero_copy_plan(uint32_t n, uint64_t total_len);
 /* The zero-copy kernel on its own (A/B probes): piece i is d_lens[i] bytes at
  * the device-visible address d_srcs[i] (HBM, or a registered host buffer's
  * device mapping), 16-byte aligned; d_digests n x 20 B, d_expected /
- * d_matched optional.  The pair form, or with VX_ZC_LOADER=1 in the
- * environment the three-wave form.  Enqueue-only on `stream` (a hipStream_t
- * or NULL). */
+ * d_matched optional.  loader = 0: the pair form, 1: the three-wave form.
+ * Enqueue-only on `stream` (a hipStream_t or NULL). */
 int vx_tuning_zero_copy_kernel(const uint64_t* d_srcs, const uint32_t* d_lens, uint32_t n, void* d_digests,
-                               const void* d_expected, void* d_matched, void* stream);
+                               const void* d_expected, void* d_matched, int loader, void* stream);
 /* Fault injection for tests: after k more successful piece submits (async or
  * inside a host batch), the next one fails with VX_ENOMEM without latching
  * the context, as a failed pinned-stage allocation does.  k < 0 turns it off. */

@@ -2,7 +2,11 @@
 // ranges that are not in the page cache), used by tests/test_native_cpu.py.
 // Not the product; no GPU.
 //
-// argv: path mode.  Reads a fixed list of ranges of the file — 4 KiB aligned
+// argv: path mode [replacement].  mode 1 = DirectIo enabled, 0 = disabled.
+// With a replacement path, that file is renamed over `path` after `path` was
+// opened and before DirectIo is built: every read must still return the
+// opened file's bytes (the O_DIRECT descriptor reopens the open file, not the
+// path).  Reads a fixed list of ranges of the file — 4 KiB aligned
 // and not, aligned and unaligned destinations, a range ending at EOF, an
 // aligned head with an unaligned tail — through DirectIo::read into a
 // page-aligned buffer, and compares each with a plain buffered pread.  Prints
@@ -21,7 +25,7 @@
 
 int main(int argc, char** argv) {
     if (argc < 3) {
-        std::fprintf(stderr, "usage: direct_check path mode\n");
+        std::fprintf(stderr, "usage: direct_check path mode [replacement]\n");
         return 2;
     }
     const char* path = argv[1];
@@ -31,8 +35,8 @@ int main(int argc, char** argv) {
     if (fd < 0 || fstat(fd, &st) != 0) return 2;
     const int64_t size = st.st_size;
     std::vector<int> fds{fd};
-    const char* paths[1] = {path};
-    vx_files::DirectIo dio(paths, fds, mode);
+    if (argc > 3 && rename(argv[3], path) != 0) return 2;  // the path now names another file
+    vx_files::DirectIo dio(fds, mode != 0);
     const double resident = dio.resident_fraction();
     const int64_t K = 4096;
     struct R {

@@ -31,7 +31,26 @@ def test_completion_layout():
 
     assert ctypes.sizeof(vx_completion) == 32
     assert vx_completion.digest.offset == 9
-    assert ctypes.sizeof(vx_config) == 24
+    assert ctypes.sizeof(vx_config) == 48
+
+
+def test_config_layout(tmp_path):
+    """vx_config (ABI 2) as ctypes has the C struct's size and every field's
+    offset: C says so, compiled here."""
+    from vortex_amd._lib import CONFIG_OPTIONS, vx_config
+
+    fields = [name for name, _ in vx_config._fields_]
+    c = tmp_path / "c.c"
+    body = ", ".join(f"offsetof(vx_config, {f})" for f in fields)
+    c.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "vx_hash.h"\nint main(void){size_t o[] = {'
+                 + body + '}; printf("%zu", sizeof(vx_config)); for (size_t i = 0; i < sizeof(o) / sizeof(o[0]); '
+                 '++i) printf(" %zu", o[i]); printf("\\n"); return 0;}\n')
+    exe = tmp_path / "c"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(c), "-o",
+                    str(exe)], check=True)
+    got = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
+    assert got == [ctypes.sizeof(vx_config)] + [getattr(vx_config, f).offset for f in fields]
+    assert fields[5:] == list(CONFIG_OPTIONS)
 
 
 def test_stats_layout(tmp_path):
@@ -65,7 +84,7 @@ def test_library_exports_declared_symbols(built):
     assert not missing, missing
     for name in decl:
         assert hasattr(lib, name)
-    assert lib.vx_abi_version() == 1
+    assert lib.vx_abi_version() == 2 == _lib.ABI_VERSION
 
 
 def test_no_cpu_fallback_in_product():
@@ -97,7 +116,17 @@ def test_validation_without_gpu(built):
     L.vx_config_default(ctypes.byref(cfg), 262144)
     assert cfg.max_piece_len == 262144 and cfg.slots >= 1 and cfg.batch_pieces >= 1
     assert cfg.slot_bytes >= 262144
+    assert (cfg.zero_copy, cfg.direct_io, cfg.batch_chunk, cfg.verify_chunk, cfg.verify_cold_chunk,
+            cfg.verify_ramp) == (1, 1, 65536, 0, 0, 1)
     h = ctypes.c_void_p()
+    # option values outside their ranges are refused before any device is looked at
+    for field, value in (("zero_copy", 2), ("direct_io", 7), ("verify_ramp", 6), ("batch_chunk", 1000),
+                         ("verify_chunk", 4097), ("verify_cold_chunk", 2048)):
+        badopt = _lib.vx_config()
+        L.vx_config_default(ctypes.byref(badopt), 262144)
+        setattr(badopt, field, value)
+        assert L.vx_create(ctypes.byref(badopt), ctypes.byref(h)) == _lib.VX_EINVAL, field
+        assert field.encode() in L.vx_last_error() or b"chunk sizes" in L.vx_last_error()
     if L.vx_device_count() == 0:
         assert L.vx_create(ctypes.byref(cfg), ctypes.byref(h)) == _lib.VX_ENODEV
     bad = _lib.vx_config()
@@ -327,3 +356,72 @@ def test_plan_verify_matches_measured_grid(built):
     for lp in grid["loop"]:  # download path: latency p50 ~ one piece's chain
         rc, p = _plan(1, lp["piece_len"], lp["piece_len"])
         assert abs(p.piece_latency_s * 1e3 / lp["latency_ms_p50"] - 1) < 0.15, lp
+
+
+def _gpu_test_option_values():
+    """Constant values each vx_config option takes in HashPool(...) calls of the
+    -m gpu tests: keyword constants, and for a keyword bound to a parametrized
+    name, the constants of that parametrize list."""
+    import ast
+
+    vals = {}
+    tdir = os.path.join(ROOT, "tests")
+    for f in sorted(os.listdir(tdir)):
+        if not (f.startswith("test_gpu") and f.endswith(".py")):
+            continue
+        tree = ast.parse(open(os.path.join(tdir, f)).read())
+        params = {}  # parametrized name -> values, file-wide (helpers take them as arguments)
+        for dec in ast.walk(tree):  # @pytest.mark.parametrize("a,b", [(..), ..])
+            if isinstance(dec, ast.Call) and getattr(dec.func, "attr", "") == "parametrize" and len(dec.args) == 2:
+                try:  # our own test files: constant arithmetic such as 2 << 20, no names
+                    names = [x.strip() for x in ast.literal_eval(dec.args[0]).split(",")]
+                    rows = eval(compile(ast.Expression(dec.args[1]), f, "eval"), {"__builtins__": {}})
+                except (ValueError, NameError, TypeError):
+                    continue
+                for row in rows:
+                    row = row if isinstance(row, tuple) else (row,)
+                    for k, v in zip(names, row):
+                        params.setdefault(k, set()).add(v)
+        for call in ast.walk(tree):
+            if isinstance(call, ast.Call) and getattr(call.func, "id", getattr(call.func, "attr", "")) == "HashPool":
+                for kw in call.keywords:
+                    if isinstance(kw.value, ast.Constant):
+                        vals.setdefault(kw.arg, set()).add(kw.value.value)
+                    elif isinstance(kw.value, ast.Name) and kw.value.id in params:
+                        vals.setdefault(kw.arg, set()).update(params[kw.value.id])
+                    elif kw.arg is None and isinstance(kw.value, ast.Name):  # **opts built from a parametrized name
+                        for name, vs in params.items():
+                            for v in vs:
+                                vals.setdefault(f"**{kw.value.id}", set()).add((name, v))
+    return vals
+
+
+def test_every_engine_option_is_tested_off_default(built):
+    """The engine takes its configuration from vx_config only:
+    no getenv anywhere in the product library's sources, and every ABI-2
+    option is exercised by some -m gpu test at a value other than
+    vx_config_default's (and so checked against the oracle there)."""
+    from vortex_amd import _lib
+
+    csrc = os.path.join(ROOT, "vortex_amd", "csrc")
+    for f in os.listdir(csrc):
+        if f.endswith((".hip", ".hpp", ".h", ".cpp", ".inc")):
+            text = open(os.path.join(csrc, f)).read()
+            assert not re.search(r"\bgetenv\s*\(|secure_getenv|environ\b", text), f
+    for f in os.listdir(os.path.join(ROOT, "vortex_amd")):
+        if f.endswith(".py"):
+            text = open(os.path.join(ROOT, "vortex_amd", f)).read()
+            assert "os.environ.get(\"VX_" not in text and "getenv(\"VX_" not in text, f
+    cfg = _lib.vx_config()
+    _lib.lib().vx_config_default(ctypes.byref(cfg), 262144)
+    vals = _gpu_test_option_values()
+    # **opts dicts: {"batch_chunk": chunk} with chunk parametrized
+    for key, pairs in vals.items():
+        if key.startswith("**"):
+            for name, v in pairs:
+                if name == "chunk" and v is not None:
+                    vals.setdefault("batch_chunk", set()).add(v)
+    for opt in _lib.CONFIG_OPTIONS:
+        default = getattr(cfg, opt)
+        tested = {v for v in vals.get(opt, set()) if isinstance(v, int)}
+        assert tested - {default}, f"vx_config.{opt}: no -m gpu test sets a non-default value (seen {tested})"

@@ -191,3 +191,24 @@ def test_clock_from_stamps():
     assert r["GHz_per_xcc"]["0"] == pytest.approx(2.0, rel=1e-6)
     assert r["GHz_per_xcc"]["7"] == pytest.approx(2.35, rel=1e-6)
     assert r["GHz_mean"] == pytest.approx(2.175, rel=1e-4) and r["span_ms"] == pytest.approx(100.0)
+
+
+@pytest.mark.gpu
+def test_reverify_multi_leg_rehearsal(built, gpu):
+    """The N>1 line's config-5 leg (bench.reverify_multi_leg), rehearsed with 2
+    gloo ranks on the box's one GPU and 5 % of linux-mint's pieces: every rank
+    verifies its piece range on its GPU, the slowest rank's time is the call's,
+    every verdict is gathered and checked (a wrong one raises on every rank),
+    and the CPU pool restatement runs beside it with every host CPU."""
+    args = ["--pieces", "1024", "--steps", "2", "--warmup", "1", "--no-e2e", "--no-ragged", "--no-cpu-baseline",
+            "--gpus", "2", "--same-device", "--dist-backend", "gloo", "--reverify-multi-scale", "0.05"]
+    r = _run(args, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    (res,) = _lines(r.stdout)
+    rm = res["reverify_multi"]
+    assert "error" not in rm, rm
+    assert rm["ranks"] == 2 and rm["same_device"] is True and rm["cpu_pool_verdicts_ok"] is True
+    assert rm["pieces"] == 70 and rm["bytes"] == 69 * 2097152 + 1179648
+    for leg in ("warm", "cold"):
+        assert rm[leg]["value"] > 0 and rm[leg]["cpu_pool"]["value"] > 0
+        assert all(len(t) == 2 for t in rm[leg]["rank_traces"])

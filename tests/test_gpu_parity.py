@@ -498,23 +498,20 @@ def test_verify_files_chunked(built, gpu, tmp_path, pl, slot_mib, batch):
     assert not all(got) and any(got)
 
 
-@pytest.mark.parametrize("chunk,ramp,pl,growth", [(65536, 1, 2 << 20, 0), (262144, 1, (1 << 20) + 3072, 0),
-                                                  (131072, 0, (1 << 20) + 3072, 0), (4096, 1, 300000, 0),
-                                                  (None, 1, 300000, 0), (None, 1, 2 << 20, 0), (None, 1, 262144, 0),
-                                                  (65536, 3, (1 << 20) + 3072, 0), (None, 1, 2 << 20, 1),
-                                                  (65536, 2, (1 << 20) + 3072, 1), (4096, 1, 300000, 1)])
-def test_verify_files_chunk_schedule(built, gpu, tmp_path, monkeypatch, chunk, ramp, pl, growth):
-    """Re-verify round schedules: other chunk sizes, and the
-    head/tail ramp (C/4, C/4, C/2 ... C/2, C/4, rest) with piece lengths that
-    are not multiples of C/4, and the x5/4 head ramp (VX_VERIFY_RAMP_GROWTH=1,
-    A/B option).  Small slots force several windows, so the ramp applies only
-    to the first and last; a range call starts mid-torrent."""
+@pytest.mark.parametrize("chunk,ramp,pl", [(65536, 1, 2 << 20), (262144, 1, (1 << 20) + 3072),
+                                           (131072, 0, (1 << 20) + 3072), (4096, 1, 300000),
+                                           (0, 1, 300000), (0, 1, 2 << 20), (0, 1, 262144),
+                                           (65536, 3, (1 << 20) + 3072), (65536, 2, (1 << 20) + 3072),
+                                           (0, 0, 2 << 20), (8192, 5, 300000)])
+def test_verify_files_chunk_schedule(built, gpu, tmp_path, chunk, ramp, pl):
+    """Re-verify round schedules: other chunk sizes
+    (vx_config.verify_chunk; 0 = the per-call policy, verify_chunk_for), and
+    the head/tail ramp of depth vx_config.verify_ramp (d = 1: C/4, C/4, C/2
+    ... C/2, C/4, rest; 0 = none) with piece lengths that are not multiples of
+    C/4.  Small slots force several windows, so the ramp applies only to the
+    first and last; a range call starts mid-torrent."""
     from vortex_amd.hash_pool import HashPool
 
-    if chunk is not None:  # None: the per-call policy (verify_chunk_for)
-        monkeypatch.setenv("VX_VERIFY_CHUNK", str(chunk))
-    monkeypatch.setenv("VX_VERIFY_RAMP", str(ramp))
-    monkeypatch.setenv("VX_VERIFY_RAMP_GROWTH", str(growth))
     sizes = [3 * pl + 777, 0, 5 * pl + 64, pl // 3]
     paths = []
     for k, L in enumerate(sizes):
@@ -525,7 +522,7 @@ def test_verify_files_chunk_schedule(built, gpu, tmp_path, monkeypatch, chunk, r
     exp = b"".join(hashlib.sha1(data[i:i + pl]).digest() for i in range(0, len(data), pl))
     n = len(exp) // 20
     slot = max(4 << 20, 3 * (chunk or 262144))  # a few pieces' chunks per window
-    with HashPool(pl, slots=3, batch_pieces=4, slot_bytes=max(slot, pl)) as pool:
+    with HashPool(pl, slots=3, batch_pieces=4, slot_bytes=max(slot, pl), verify_chunk=chunk, verify_ramp=ramp) as pool:
         got, bad = pool.verify_files(paths, sizes, pl, exp, io_threads=3)
         assert got == [True] * n and bad == 0
         with open(paths[2], "r+b") as f:  # flip a byte in the last C/4 of a piece
@@ -700,18 +697,18 @@ def _strided_pieces(buf, n, L, hs, last_len):
     (300 * 1024, 0, 1, None, 8, None),                       # a single piece
     (256 * 1024, 0, 257, 64, 4, 128 * 1024),                 # last piece shorter than one block
 ])
-def test_strided_batch_chunked(built, gpu, monkeypatch, L, hs_extra, n, last_len, slot_mib, chunk):
+def test_strided_batch_chunked(built, gpu, L, hs_extra, n, last_len, slot_mib, chunk):
     """Strided host batches of long pieces take the resumable chunk path
-    (one hipMemcpy2DAsync per round): digests and verdicts
-    bit-exact vs hashlib/the oracle, identical to the whole-piece path
-    (VX_BATCH_CHUNK=0), and the chunk path really ran."""
+    (one hipMemcpy2DAsync per round; vx_config.batch_chunk,
+    None = the default 64 KiB): digests and verdicts bit-exact vs hashlib/the
+    oracle, identical to the whole-piece path (batch_chunk=0), and the chunk
+    path really ran."""
     import mmap
 
     from vortex_amd import _lib
     from vortex_amd.hash_pool import HashPool
 
-    if chunk is not None:
-        monkeypatch.setenv("VX_BATCH_CHUNK", str(chunk))
+    opts = {} if chunk is None else {"batch_chunk": chunk}
     last_len = L if last_len is None else last_len
     hs = L + hs_extra
     buf = mmap.mmap(-1, (n - 1) * hs + last_len)
@@ -724,7 +721,7 @@ def test_strided_batch_chunked(built, gpu, monkeypatch, L, hs_extra, n, last_len
     bad = {n // 2, n - 1} if n > 1 else {0}
     for i in bad:
         exp[i] = bytes(20)
-    with HashPool(L, slots=3, slot_bytes=slot_mib << 20) as pool:
+    with HashPool(L, slots=3, slot_bytes=slot_mib << 20, **opts) as pool:
         pool.register_buffer(buf)
         r0 = _lib.lib().vx_tuning_chunk_rounds(pool._h)
         dig = pool.sha1_batch(pieces)
@@ -735,8 +732,7 @@ def test_strided_batch_chunked(built, gpu, monkeypatch, L, hs_extra, n, last_len
     assert matched == [i not in bad for i in range(n)]
     assert rounds >= 2 * ((L + (chunk or 65536) - 1) // (chunk or 65536))
     # the whole-piece path on the same pieces agrees (and takes no chunk rounds)
-    monkeypatch.setenv("VX_BATCH_CHUNK", "0")
-    with HashPool(L, slots=3, slot_bytes=slot_mib << 20) as pool:
+    with HashPool(L, slots=3, slot_bytes=slot_mib << 20, batch_chunk=0) as pool:
         pool.register_buffer(buf)
         matched0, dig0 = pool.verify_batch(pieces, exp)
         assert _lib.lib().vx_tuning_chunk_rounds(pool._h) == 0
@@ -744,21 +740,18 @@ def test_strided_batch_chunked(built, gpu, monkeypatch, L, hs_extra, n, last_len
     assert matched0 == matched and dig0 == want
 
 
-@pytest.mark.parametrize("gather", ["1", "0"])
-def test_scattered_registered_pieces(built, gpu, monkeypatch, gather):
+def test_scattered_registered_pieces(built, gpu):
     """Pieces scattered over a registered pool (buf_pool.rs buffers in no
     particular order) are pulled by the gather kernel on the
     async path and on non-strided host batches; unaligned registered pieces
     fall back to per-piece DMA and unregistered ones to the pinned stage, all
-    in the same batches.  Digests bit-exact vs hashlib/the oracle with the
-    gather kernel on and off (VX_GATHER)."""
+    in the same batches.  Digests bit-exact vs hashlib/the oracle.
+    (zero_copy=0: the gather path itself; zero-copy slots: test_gpu_zero_copy.py)"""
     import mmap
 
     from vortex_amd import _lib
     from vortex_amd.hash_pool import HashPool
 
-    monkeypatch.setenv("VX_GATHER", gather)
-    monkeypatch.setenv("VX_ZERO_COPY", "0")  # the gather path itself (zero-copy slots: test_gpu_zero_copy.py)
     rng = random.Random(5)
     lens = [0, 1, 15, 16, 17, 63, 64, 65, 4095, 65535, 65536, 65537, 131072 + 48, 200000, (1 << 20) + 3, 300]
     lens = lens * 6
@@ -777,7 +770,7 @@ def test_scattered_registered_pieces(built, gpu, monkeypatch, gather):
     allp = pieces + extra
     want = [hashlib.sha1(p).digest() for p in allp]
     assert want[3] == oracle.sha1(bytes(allp[3]))
-    with HashPool(1 << 21, slots=3, batch_pieces=24, slot_bytes=8 << 20) as pool:
+    with HashPool(1 << 21, slots=3, batch_pieces=24, slot_bytes=8 << 20, zero_copy=0) as pool:
         pool.register_buffer(buf)
         t0 = _lib.lib().vx_tuning_gather_tiles(pool._h)
         for i, p in enumerate(allp):
@@ -795,7 +788,7 @@ def test_scattered_registered_pieces(built, gpu, monkeypatch, gather):
         assert got[i][0] == (i % 9 != 0), i
     assert dig == want
     expect_tiles = 2 * sum((L + 65535) // 65536 for k, L in enumerate(lens) if k % 7 and L)
-    assert tiles == (expect_tiles if gather == "1" else 0)
+    assert tiles == expect_tiles
 
 
 def test_lazy_flush_launches_from_poll(built, gpu):
@@ -827,7 +820,7 @@ def test_lazy_flush_launches_from_poll(built, gpu):
 
 
 @pytest.mark.parametrize("chunk", [None, 32 * 1024])
-def test_gather_batch_chunked(built, gpu, monkeypatch, chunk):
+def test_gather_batch_chunked(built, gpu, chunk):
     """A host batch whose pieces sit in separately registered buffers (vortex's
     BufferPool: one mmap per buffer, buf_pool.rs:92-98), ragged lengths with
     the longest >= 2 chunks, takes the chunked gather path:
@@ -838,8 +831,7 @@ def test_gather_batch_chunked(built, gpu, monkeypatch, chunk):
     from vortex_amd import _lib
     from vortex_amd.hash_pool import HashPool
 
-    if chunk is not None:
-        monkeypatch.setenv("VX_BATCH_CHUNK", str(chunk))
+    opts = {} if chunk is None else {"batch_chunk": chunk}
     rng = random.Random(11)
     lens = [(1 << 20) + 3, 262144, 0, 64, 200000, 131072 + 16, 5, (1 << 20), 700000] * 5
     rng.shuffle(lens)
@@ -852,7 +844,7 @@ def test_gather_batch_chunked(built, gpu, monkeypatch, chunk):
     want = [hashlib.sha1(p).digest() for p in pieces]
     assert want[1] == oracle.sha1(bytes(pieces[1]))
     exp = [w if i % 7 else bytes(20) for i, w in enumerate(want)]
-    with HashPool(max(lens), slots=3, slot_bytes=4 << 20) as pool:  # 4 MiB slots: several windows
+    with HashPool(max(lens), slots=3, slot_bytes=4 << 20, **opts) as pool:  # 4 MiB slots: several windows
         for b in bufs:
             pool.register_buffer(b)
         r0 = _lib.lib().vx_tuning_chunk_rounds(pool._h)
@@ -868,8 +860,7 @@ def test_gather_batch_chunked(built, gpu, monkeypatch, chunk):
     C = chunk or 65536
     assert rounds > 0
     assert tiles == 2 * sum((L + C - 1) // C for L in lens)  # one tile per chunk (C <= 64 KiB)
-    monkeypatch.setenv("VX_BATCH_CHUNK", "0")
-    with HashPool(max(lens), slots=3, slot_bytes=4 << 20) as pool:
+    with HashPool(max(lens), slots=3, slot_bytes=4 << 20, batch_chunk=0) as pool:
         matched0, dig0 = pool.verify_batch(pieces, exp)  # unregistered: whole-piece staged path
         assert _lib.lib().vx_tuning_chunk_rounds(pool._h) == 0
     assert matched0 == matched and dig0 == want
@@ -920,21 +911,19 @@ def test_pool_growth_mid_flight(built, gpu):
         assert r.hash_matched == (i % 5 != 0), i
 
 
-@pytest.mark.parametrize("sort", ["1", "0"])
-def test_ragged_host_batch_streaming(built, gpu, monkeypatch, sort):
+def test_ragged_host_batch_streaming(built, gpu):
     """A shuffled ragged host batch (config 3's shape, scaled down) in one
     registered mmap takes the chunked gather path.  Longest-first streaming
-    rounds (VX_BATCH_SORT=1) admit short pieces into the long
-    pieces' later rounds and small slots force the lane limit; caller-order
-    windows (=0) are the A/B baseline.  Both must give hashlib's digests and
-    the expected verdicts, moving each chunk exactly once; the same batch in
-    plain memory (whole-piece slots, longest first) must agree too."""
+    rounds admit short pieces into the long pieces' later
+    rounds and small slots force the lane limit.  It must give hashlib's
+    digests and the expected verdicts, moving each chunk exactly once; the
+    same batch in plain memory (whole-piece slots, longest first) must agree
+    too."""
     import mmap
 
     from vortex_amd import _lib
     from vortex_amd.hash_pool import HashPool
 
-    monkeypatch.setenv("VX_BATCH_SORT", sort)
     rng = random.Random(31)
     lens = [(1 << 20) + 48] * 3 + [1 << 20] * 2 + [200000 + 16 * k for k in range(30)] + [16384] * 700 + \
         [0, 16, 64, 4096, 65536, 65552] + [16 * rng.randint(1, 4096) for _ in range(300)]

@@ -161,16 +161,19 @@ def test_verify_files_multi_contexts(built, gpu, tmp_path, nctx, pl):
             p.close()
 
 
-@pytest.mark.parametrize("pl,cold_chunk", [(256 * 1024, 0), (2 << 20, 0), (2 << 20, 1 << 20), (4 << 20, 1 << 20)])
-def test_verify_files_cold_direct_reads(built, gpu, tmp_path, monkeypatch, pl, cold_chunk):
+@pytest.mark.parametrize("pl,cold_chunk,direct_io", [(256 * 1024, 0, 1), (2 << 20, 0, 1), (2 << 20, 1 << 20, 1),
+                                                     (4 << 20, 1 << 20, 1), (2 << 20, 0, 0), (256 * 1024, 0, 0)])
+def test_verify_files_cold_direct_reads(built, gpu, tmp_path, pl, cold_chunk, direct_io):
     """Re-verify of files whose pages are NOT in the page cache: the readers
     take the O_DIRECT path for aligned, uncached ranges (vx_files::DirectIo,
     DESIGN.md §6.1) and the buffered path for the rest (unaligned segments
     where files meet, a short tail).  Verdicts equal the oracle's on the same
     damaged multi-file torrent, and the call's trace shows direct reads when
-    the filesystem takes O_DIRECT.  With VX_VERIFY_COLD_CHUNK (off by
+    the filesystem takes O_DIRECT.  With vx_config.verify_cold_chunk (off by
     default) evicted calls of pieces >= 2 MiB run 1 MiB rounds (many windows
-    of the 16 MiB slots); cached ones, and every call by default, 256 KiB."""
+    of the 16 MiB slots); cached ones, and every call by default, 256 KiB.
+    With direct_io = 0 every read goes through the page cache (vortex's own
+    pread) and the verdicts are the same."""
     import pathlib
     import shutil
     import tempfile
@@ -191,13 +194,13 @@ def test_verify_files_cold_direct_reads(built, gpu, tmp_path, monkeypatch, pl, c
     direct_ok = takes_direct(str(where))
     print(f"cold re-verify test dir {where}: O_DIRECT {'yes' if direct_ok else 'no'}")
     try:
-        _cold_direct_reads(where, pl, cold_chunk, direct_ok, monkeypatch)
+        _cold_direct_reads(where, pl, cold_chunk, direct_ok, direct_io)
     finally:
         if own:
             shutil.rmtree(own, ignore_errors=True)
 
 
-def _cold_direct_reads(tmp_path, pl, cold_chunk, direct_ok, monkeypatch):
+def _cold_direct_reads(tmp_path, pl, cold_chunk, direct_ok, direct_io):
     from vortex_amd.hash_pool import HashPool
 
     sizes = [3 * pl + 4096 * 3, 5 * pl, 2 * pl + 777, pl + 1, 9 * pl]  # aligned and misaligned file starts
@@ -217,19 +220,18 @@ def _cold_direct_reads(tmp_path, pl, cold_chunk, direct_ok, monkeypatch):
             os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
             os.close(fd)
 
-    if cold_chunk:
-        monkeypatch.setenv("VX_VERIFY_COLD_CHUNK", str(cold_chunk))
-    else:
-        monkeypatch.delenv("VX_VERIFY_COLD_CHUNK", raising=False)
     chunked = pl >= 2 << 20
-    with HashPool(pl, slots=3, slot_bytes=16 << 20) as pool:
+    with HashPool(pl, slots=3, slot_bytes=16 << 20, verify_cold_chunk=cold_chunk, direct_io=direct_io) as pool:
         for _ in range(2):
             evict()
             got, bad = pool.verify_files(paths, sizes, pl, exp, io_threads=4)
             assert got == want and bad == 0
             tr = pool.last_verify()
             assert tr["read_bytes"] == sum(sizes)
-            if direct_ok:
+            if not direct_io:
+                assert tr["direct_bytes"] == 0
+                assert tr["chunk_bytes"] == (256 * 1024 if chunked else 0), tr
+            elif direct_ok:
                 assert tr["direct_bytes"] > 0
                 assert tr["chunk_bytes"] == ((cold_chunk or 256 * 1024) if chunked else 0), tr
         # cached now (the buffered reads above filled part of it; read the rest): no direct reads

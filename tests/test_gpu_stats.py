@@ -27,14 +27,13 @@ def _check_latency(st):
         assert st["batch_latency_max_us"] >> top in (1, 0) or top == len(st["batch_latency_hist"]) - 1
 
 
-def test_stats_async_path(built, gpu, monkeypatch):
+def test_stats_async_path(built, gpu):
     from vortex_amd.hash_pool import HashPool
-
-    monkeypatch.setenv("VX_ZERO_COPY", "0")  # counts the gather kernel's tiles (zero-copy: test_gpu_zero_copy.py)
 
     rng = random.Random(8)
     plen = 16384 * 3 + 96  # 16-byte multiple: registered pieces go through the gather kernel
-    with HashPool(plen, slots=2, batch_pieces=7) as pool:
+    # zero_copy=0: counts the gather kernel's tiles (zero-copy slots: test_gpu_zero_copy.py)
+    with HashPool(plen, slots=2, batch_pieces=7, zero_copy=0) as pool:
         st0 = pool.stats()
         assert all(v == 0 for k, v in st0.items() if k != "batch_latency_hist")
         pinned = mmap.mmap(-1, plen * 40)

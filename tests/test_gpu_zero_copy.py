@@ -1,4 +1,6 @@
-"""The zero-copy slot path (VX_ZERO_COPY=0 turns it off, anything else is the default; VX_ZC_LOADER picks the pair or the three-wave form): a slot whose
+"""The zero-copy slot path (vx_config.zero_copy = 1, the
+default; slots of fewer than 128 pieces take the three-wave form, larger ones
+the pair): a slot whose
 pieces are all registered and 16-byte aligned is hashed straight out of host
 memory by sha1_zc_split_kernel (cooperative 16-lane loads, LDS transpose),
 with no gather kernel.  Every digest and verdict must equal hashlib's / the
@@ -52,69 +54,70 @@ def _run_async(pool, pieces, want, bad_every=9, flush_every=10, table=False):
     return {r.index: (r.hash_matched, r.digest) for r in pool.try_iter()}
 
 
-@pytest.mark.parametrize("loader", ["0", "1"])  # the pair / the three-wave form
-def test_zero_copy_async_ragged_exact(built, gpu, monkeypatch, loader):
+# (batch_pieces, flush_every): 40-piece slots flushed every 10 pieces take the
+# three-wave form; one 160-piece slot launched by the drain takes the pair
+@pytest.mark.parametrize("form,batch,flush_every", [("loader", 40, 10), ("pair", 160, 1000)])
+def test_zero_copy_async_ragged_exact(built, gpu, form, batch, flush_every):
     from vortex_amd import _lib
     from vortex_amd.hash_pool import HashPool
 
-    monkeypatch.setenv("VX_ZERO_COPY", "1")
-    monkeypatch.setenv("VX_ZC_LOADER", loader)
     lens = EDGE * 5
     random.Random(3).shuffle(lens)
     buf, pieces = _pool_pieces(lens, 11)
     want = [hashlib.sha1(p).digest() for p in pieces]
     assert want[5] == oracle.sha1(bytes(pieces[5]))
-    with HashPool(2 << 20, slots=3, batch_pieces=40, slot_bytes=16 << 20) as pool:
+    with HashPool(2 << 20, slots=3, batch_pieces=batch, slot_bytes=16 << 20) as pool:
         pool.register_buffer(buf)
         z0 = _lib.lib().vx_tuning_zero_copy_slots(pool._h)
         t0 = _lib.lib().vx_tuning_gather_tiles(pool._h)
-        got = _run_async(pool, pieces, want)
+        got = _run_async(pool, pieces, want, flush_every=flush_every)
         zc = _lib.lib().vx_tuning_zero_copy_slots(pool._h) - z0
+        zl = _lib.lib().vx_tuning_zero_copy_loader_slots(pool._h)
         tiles = _lib.lib().vx_tuning_gather_tiles(pool._h) - t0
         pool.unregister_buffer(buf)
     assert len(got) == len(pieces)
     for i in range(len(pieces)):
         assert got[i][1] == want[i], (i, len(pieces[i]))
         assert got[i][0] == (i % 9 != 0), i
-    assert zc >= len(pieces) // 40 and tiles == 0  # every slot zero-copy, no gather
+    assert zc >= len(pieces) // batch and tiles == 0  # every slot zero-copy, no gather
+    assert (zl == zc) if form == "loader" else (zl < zc)
 
 
-@pytest.mark.parametrize("loader", ["0", "1"])
-def test_zero_copy_piece_table_and_batch(built, gpu, monkeypatch, loader):
+@pytest.mark.parametrize("batch", [64, 256])  # the three-wave form / the pair
+def test_zero_copy_piece_table_and_batch(built, gpu, batch):
     """The device piece table (vx_submit_piece) on zero-copy slots, and a
-    synchronous batch of short pieces (the slot path of vx_sha1_batch)."""
+    synchronous batch of short pieces (the slot path of vx_sha1_batch, which
+    goes zero-copy too: vx_hash.h)."""
     from vortex_amd import _lib
     from vortex_amd.hash_pool import HashPool
 
-    monkeypatch.setenv("VX_ZERO_COPY", "1")
-    monkeypatch.setenv("VX_ZC_LOADER", loader)
     lens = [65536] * 200 + [1000, 64, 0, 65536 - 7]
     buf, pieces = _pool_pieces(lens, 12)
     want = [hashlib.sha1(p).digest() for p in pieces]
     table = bytearray(b"".join(want))
     for i in range(0, len(lens), 13):  # these must mismatch
         table[20 * i] ^= 1
-    with HashPool(1 << 16, slots=4, batch_pieces=64) as pool:
+    with HashPool(1 << 16, slots=4, batch_pieces=batch) as pool:
         pool.register_buffer(buf)
         pool.set_piece_table(bytes(table))
         z0 = _lib.lib().vx_tuning_zero_copy_slots(pool._h)
-        got = _run_async(pool, pieces, want, table=True, flush_every=17)
+        got = _run_async(pool, pieces, want, table=True, flush_every=17 if batch == 64 else 1000)
+        z1 = _lib.lib().vx_tuning_zero_copy_slots(pool._h)
         dig = pool.sha1_batch(pieces)
         zc = _lib.lib().vx_tuning_zero_copy_slots(pool._h) - z0
         pool.unregister_buffer(buf)
     for i in range(len(pieces)):
         assert got[i] == (i % 13 != 0, want[i]), i
     assert dig == want
-    assert zc > 0
+    assert z1 > z0 and zc > z1 - z0  # the async slots and the host batch's slots
 
 
-def test_zero_copy_mixed_slots_fall_back(built, gpu, monkeypatch):
+def test_zero_copy_mixed_slots_fall_back(built, gpu):
     """Unaligned registered pieces and unregistered ones keep a slot off the
     zero-copy kernel (gather / DMA / stage as before); results stay exact."""
     from vortex_amd import _lib
     from vortex_amd.hash_pool import HashPool
 
-    monkeypatch.setenv("VX_ZERO_COPY", "1")
     lens = EDGE * 3
     random.Random(4).shuffle(lens)
     buf, pieces = _pool_pieces(lens, 13, align_every=7)
@@ -132,14 +135,13 @@ def test_zero_copy_mixed_slots_fall_back(built, gpu, monkeypatch):
     assert tiles > 0
 
 
-def test_zero_copy_config1_shape(built, gpu, monkeypatch):
+def test_zero_copy_config1_shape(built, gpu):
     """Config 1's shape on the zero-copy path: 1,024 x 256 KiB synthetic
     pieces in separately registered mmaps, shuffled, 1 % corrupted, against
     the oracle's pool."""
     from vortex_amd import _lib
     from vortex_amd.hash_pool import HashPool
 
-    monkeypatch.setenv("VX_ZERO_COPY", "1")
     n, plen, seed, every = 1024, 256 * 1024, 0x5EED0001, 100
     bufs = []
     for i in range(n):
@@ -169,20 +171,23 @@ def test_zero_copy_config1_shape(built, gpu, monkeypatch):
         assert got[i][0] == (0 if oracle.is_corrupt(i, every) else 1), i
 
 
-@pytest.mark.parametrize("plen,batch,expect_zc", [(16384, 128, True), (262144, 128, True), (2 << 20, 128, True),
-                                                  (16384, 32, True), (262144, 32, True)])
-def test_zero_copy_default_policy(built, gpu, monkeypatch, plen, batch, expect_zc):
-    """By default (VX_ZERO_COPY unset) a slot of registered aligned pieces
-    goes zero-copy at every length and batch size (vx_engine.hip launch_slot_impl;
-    small batches in the three-wave form) and never touches the gather."""
+@pytest.mark.parametrize("plen,batch,zero_copy", [(16384, 128, 1), (262144, 128, 1), (2 << 20, 128, 1),
+                                                  (16384, 32, 1), (262144, 32, 1), (262144, 128, 0), (16384, 32, 0)])
+def test_zero_copy_default_policy(built, gpu, plen, batch, zero_copy):
+    """With zero_copy = 1 (vx_config_default) a slot of registered aligned
+    pieces goes zero-copy at every length and batch size (vx_engine.hip
+    launch_slot_impl; small batches in the three-wave form) and never touches
+    the gather; with zero_copy = 0 the same pieces are gathered into HBM
+    first.  Every digest and verdict is hashlib's either way."""
     from vortex_amd import _lib
     from vortex_amd.hash_pool import HashPool
 
-    monkeypatch.delenv("VX_ZERO_COPY", raising=False)
     n = 256
+    expect_zc = zero_copy == 1
     buf, pieces = _pool_pieces([plen] * n, 21)
     want = [hashlib.sha1(p).digest() for p in pieces]
-    with HashPool(plen, slots=3, batch_pieces=batch, slot_bytes=max(128 << 20, batch * plen)) as pool:
+    with HashPool(plen, slots=3, batch_pieces=batch, slot_bytes=max(128 << 20, batch * plen),
+                  zero_copy=zero_copy) as pool:
         pool.register_buffer(buf)
         got = _run_async(pool, pieces, want, flush_every=batch)
         zc = _lib.lib().vx_tuning_zero_copy_slots(pool._h)

@@ -113,11 +113,13 @@ def _disk_dir(tmp_path):
 
 def test_direct_reads_of_uncached_ranges(tmp_path):
     """vx_files::DirectIo (the re-verify's O_DIRECT path, DESIGN.md §6.1):
-    every read returns the file's bytes whatever the alignment; ranges not in
-    the page cache go O_DIRECT (mode 1: mincore probe; mode 3: RWF_NOWAIT
-    read first) and cached ones do not; mode 0 never, mode 2 whenever aligned.
+    every read returns the file's bytes whatever the alignment; with it
+    enabled (vx_config.direct_io = 1) ranges not in the page cache go O_DIRECT
+    (mincore probe) and cached ones do not; disabled, nothing does.
     resident_fraction (which picks the re-verify's cold chunk) is ~0 on the
-    evicted file, 1 on the cached one, and 1 when nothing is mapped (mode 0)."""
+    evicted file, 1 on the cached one, and 1 when nothing is mapped.  A file
+    renamed over the path after it was opened does not leak into the reads:
+    the direct descriptor reopens the open file."""
     d = _disk_dir(tmp_path)
     if d is None:
         pytest.skip("no filesystem here takes O_DIRECT")
@@ -132,7 +134,7 @@ def test_direct_reads_of_uncached_ranges(tmp_path):
             f.flush()
             os.fsync(f.fileno())
 
-        def run(mode, evict):
+        def run(mode, evict, replacement=None):
             fd = os.open(path, os.O_RDONLY)
             if evict:
                 os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
@@ -140,7 +142,9 @@ def test_direct_reads_of_uncached_ranges(tmp_path):
                 while os.read(fd, 1 << 20):  # fault every page in
                     pass
             os.close(fd)
-            out = subprocess.run([str(exe), path, str(mode)], capture_output=True, text=True, check=True, timeout=60)
+            extra = [replacement] if replacement else []
+            out = subprocess.run([str(exe), path, str(mode)] + extra, capture_output=True, text=True, check=True,
+                                 timeout=60)
             res = json.loads(out.stdout)
             assert res["reads"] >= 9 and res["mismatches"] == 0, res
             resident.append(res["resident"])
@@ -153,13 +157,16 @@ def test_direct_reads_of_uncached_ranges(tmp_path):
         warm = run(1, evict=False)
         assert resident[-1] == 1.0
         assert warm == 0  # cached: buffered
-        forced = run(2, evict=False)
-        assert forced > 0
         # evicted pages read direct (the kernel may keep a few pages; most ranges go direct)
         assert cold > 0
-        # mode 3: RWF_NOWAIT from the page cache, O_DIRECT for what it could not return
-        assert run(3, evict=False) == 0
-        assert run(3, evict=True) > 0
+        # another file renamed over the path after the open: reads still match the opened file
+        other = path + ".new"
+        with open(other, "wb") as f:
+            f.write(os.urandom((8 << 20) + 12345))
+            f.flush()
+            os.fsync(f.fileno())
+        assert run(1, evict=True, replacement=other) > 0  # direct reads happened, and none mismatched
     finally:
-        if os.path.exists(path):
-            os.unlink(path)
+        for p in (path, path + ".new"):
+            if os.path.exists(p):
+                os.unlink(p)

@@ -103,7 +103,7 @@ def main():
         "runs_GiBps": [round(total / r / GiB, 2) for r in runs],
         "ms": round(el * 1e3, 1),
         "cpu_pool_GiBps": round(total / t_cpu / GiB, 2), "cpu_threads": threads, "sha_ni": bool(oracle.has_shani()),
-        "registered": not a.unregistered, "VX_BATCH_SORT": os.environ.get("VX_BATCH_SORT", "1"),
+        "registered": not a.unregistered,
         "register_s": round(t_reg, 2), "gen_s": round(t_gen, 2),
         "checked": "all verdicts and digests equal to the CPU pool restatement",
     }), flush=True)

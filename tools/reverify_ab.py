@@ -2,15 +2,16 @@
 """A/B of the config-5 re-verify pipeline, warm and cold.
 
 Writes the linux-mint-geometry file once (fsync'd, on a disk-backed
-filesystem: bench.reverify_dir), then for every engine configuration (env
-knobs read at vx_create) runs `--reps` warm calls and `--cold-reps` calls
+filesystem: bench.reverify_dir), then for every engine configuration
+(vx_config options, vortex_amd._lib.CONFIG_OPTIONS) runs `--reps` warm calls and `--cold-reps` calls
 after evicting the file (fsync + POSIX_FADV_DONTNEED), alternating
 configurations per rep so box drift hits all of them alike.  Prints one JSON
 line per configuration with the GiB/s runs and each call's
 vx_tuning_last_verify budget, and the CPU pool on the same file.
 
 usage: python tools/reverify_ab.py [--reps 3] [--cold-reps 2] [--configs name=K=V,K=V;...]
-A configuration's IO_THREADS=N (not an engine knob) sets its io_threads
+e.g. --configs "default=;cold1m=verify_cold_chunk=1048576;buffered=direct_io=0".
+A configuration's IO_THREADS=N (not a vx_config field) sets its io_threads
 (default: the process's CPU share).
 """
 import argparse
@@ -22,15 +23,15 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-DEFAULT = "default=;whole=VX_VERIFY_CHUNKED_ABOVE=4194304;ra3=VX_VERIFY_READAHEAD=3;mode3=VX_H2D_MODE=3"
+DEFAULT = "default=;buffered=direct_io=0"
 
 
 def parse(spec):
     out = []
     for item in spec.split(";"):
         name, _, kv = item.partition("=")
-        env = dict(p.split("=", 1) for p in kv.split(",") if p)
-        out.append((name, env))
+        opts = dict(p.split("=", 1) for p in kv.split(",") if p)
+        out.append((name, opts))
     return out
 
 
@@ -59,8 +60,8 @@ def main():
     buf = ctypes.create_string_buffer(pl)
     configs = parse(a.configs)
     io = {name: int(env.pop("IO_THREADS", 0)) or threads for name, env in configs}
-    res = {name: {"warm": [], "cold": [], "warm_tr": [], "cold_tr": [], "env": env, "io_threads": io[name]}
-           for name, env in configs}
+    res = {name: {"warm": [], "cold": [], "warm_tr": [], "cold_tr": [], "options": opts, "io_threads": io[name]}
+           for name, opts in configs}
     cpu = {"warm": [], "cold": []}
     try:
         with open(path, "wb") as f:
@@ -73,15 +74,9 @@ def main():
         exp = oracle.pool_digest_synth(0x5EED0005, 0, n, pl, last_index=n - 1, last_len=last, threads=threads)
         cache_nodes = page_cache_nodes(path)
         pools = {}
-        for name, env in configs:
-            saved = {k: os.environ.get(k) for k in env}
-            os.environ.update(env)
-            pools[name] = HashPool(pl, slots=4, slot_bytes=512 << 20, batch_pieces=4096)
-            for k, v in saved.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
+        for name, opts in configs:
+            pools[name] = HashPool(pl, slots=4, slot_bytes=512 << 20, batch_pieces=4096,
+                                   **{k: int(v, 0) for k, v in opts.items()})
             got, bad = pools[name].verify_files([path], [total], pl, exp, io_threads=io[name])  # warm-up
             assert all(got) and bad == 0
         for leg, reps in (("warm", a.reps), ("cold", a.cold_reps)):

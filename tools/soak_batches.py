@@ -3,8 +3,8 @@
 fixed time: random ragged batches (empty to 5 MiB pieces, shuffled), held in
 one registered mmap (strided or gather paths), in separately registered
 buffers, at unaligned addresses, or in plain memory (parallel stage copies),
-with random slot counts and sizes, planted mismatches, and the longest-first
-scheduler on or off (VX_BATCH_SORT, read at vx_create).  Every digest and
+with random slot counts and sizes, chunk sizes (vx_config.batch_chunk, 0 =
+whole-piece slots) and planted mismatches.  Every digest and
 verdict is checked against the CPU pool restatement (oracle/, the checker).
 Prints a progress line per pool and one JSON line at the end; exits non-zero
 on any difference.
@@ -39,13 +39,13 @@ def main():
     t_end = time.time() + a.seconds
     st = {"pools": 0, "batches": 0, "pieces": 0, "GiB": 0.0, "mismatches_planted": 0}
     while time.time() < t_end:
-        os.environ["VX_BATCH_SORT"] = rng.choice(["1", "1", "0"])
+        batch_chunk = rng.choice([65536, 65536, 32768, 131072, 0])
         max_len = rng.choice([1 << 16, 1 << 20, 3 << 20, 5 << 20])
         classes = [0, 1, 63, 64, 65, 16384, 65536, 65537, 200000, 262144, 1 << 20, (1 << 20) + 48, 3 << 20, 5 << 20]
         classes = [L for L in classes if L <= max_len]
         slots = rng.choice([2, 3, 4])
         slot_bytes = rng.choice([None, max(max_len, 4 << 20), max(max_len, 64 << 20)])
-        with HashPool(max_len, slots=slots, slot_bytes=slot_bytes) as pool:
+        with HashPool(max_len, slots=slots, slot_bytes=slot_bytes, batch_chunk=batch_chunk) as pool:
             st["pools"] += 1
             for _ in range(rng.randint(1, 4)):
                 n = rng.randint(1, 600)
@@ -87,7 +87,7 @@ def main():
                     pool.unregister_buffer(b)
                 if not ok:
                     print(json.dumps({"ok": False, "seed": a.seed, "mode": mode, "lens": lens,
-                                      "VX_BATCH_SORT": os.environ["VX_BATCH_SORT"]}), flush=True)
+                                      "batch_chunk": batch_chunk}), flush=True)
                     return 1
                 st["batches"] += 1
                 st["pieces"] += n

@@ -29,6 +29,7 @@ sys.path.insert(0, ROOT)
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--loader", type=int, default=0, help="0: the zero-copy pair, 1: the three-wave form")
     a = ap.parse_args()
     import torch
 
@@ -62,7 +63,7 @@ def main() -> None:
             else:
                 srcs = src_hbm if kind == "zc_hbm" else src_host
                 check(lib().vx_tuning_zero_copy_kernel(srcs.data_ptr(), lens.data_ptr(), n, digs[kind].data_ptr(),
-                                                       None, None, int(st.cuda_stream)), "zc kernel")
+                                                       None, None, a.loader, int(st.cuda_stream)), "zc kernel")
 
         res = {"pieces": n, "piece_len": plen}
         blocks = (plen + 9 + 63) // 64

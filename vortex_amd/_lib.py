@@ -15,10 +15,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# VX_LIB_OVERRIDE: A/B tooling only (tools/gpu_ab_builds.sh runs two builds of
-# the engine on one box, alternating processes); the product loads the in-tree
-# build.
-LIB_PATH = os.environ.get("VX_LIB_OVERRIDE") or os.path.join(_HERE, "libvortex_amd.so")
+LIB_PATH = os.path.join(_HERE, "libvortex_amd.so")
 
 VX_OK = 0
 VX_EINVAL = -22
@@ -37,7 +34,7 @@ EXPORTS = (
     "vx_sha1_batch", "vx_verify_batch", "vx_verify_files", "vx_verify_files_range", "vx_verify_files_multi",
     "vx_sha1_device_uniform", "vx_sha1_device_ragged", "vx_sha1_device_ragged_hint", "vx_sort_order",
     "vx_synth_fill", "vx_sha1_device_uniform_variant", "vx_sha1_device_ragged_variant",
-    "vx_tuning_chunk_rounds", "vx_tuning_gather_tiles", "vx_tuning_zero_copy_slots", "vx_tuning_zero_copy_plan", "vx_tuning_zero_copy_kernel", "vx_tuning_plan_ragged", "vx_tuning_chunk_schedule",
+    "vx_tuning_chunk_rounds", "vx_tuning_gather_tiles", "vx_tuning_zero_copy_slots", "vx_tuning_zero_copy_loader_slots", "vx_tuning_zero_copy_plan", "vx_tuning_zero_copy_kernel", "vx_tuning_plan_ragged", "vx_tuning_chunk_schedule",
     "vx_tuning_fail_submit_after", "vx_plan_verify", "vx_plan_verify_gpus", "vx_get_stats", "vx_reset_stats",
     "vx_tuning_fail_launch_after", "vx_tuning_last_verify", "vx_tuning_clock_stamp", "vx_tuning_wall_clock_khz",
     "vx_tuning_device_identity",
@@ -57,9 +54,16 @@ class vx_completion(ctypes.Structure):
                 ("_pad", ctypes.c_uint8 * 3)]
 
 
+ABI_VERSION = 2
+
+# vx_config fields a caller may set beyond the pool geometry (ABI 2; include/vx_hash.h)
+CONFIG_OPTIONS = ("zero_copy", "direct_io", "batch_chunk", "verify_chunk", "verify_cold_chunk", "verify_ramp")
+
+
 class vx_config(ctypes.Structure):
     _fields_ = [("device", ctypes.c_int32), ("max_piece_len", ctypes.c_uint32), ("batch_pieces", ctypes.c_uint32),
-                ("slots", ctypes.c_uint32), ("slot_bytes", ctypes.c_uint64)]
+                ("slots", ctypes.c_uint32), ("slot_bytes", ctypes.c_uint64)] + \
+        [(name, ctypes.c_uint32) for name in CONFIG_OPTIONS]
 
 
 class vx_plan(ctypes.Structure):
@@ -130,8 +134,9 @@ def _declare(L: ctypes.CDLL) -> None:
         "vx_tuning_chunk_rounds": ([vp], c.c_uint64),
         "vx_tuning_gather_tiles": ([vp], c.c_uint64),
         "vx_tuning_zero_copy_slots": ([vp], c.c_uint64),
+        "vx_tuning_zero_copy_loader_slots": ([vp], c.c_uint64),
         "vx_tuning_zero_copy_plan": ([c.c_uint32, c.c_uint64], c.c_int),
-        "vx_tuning_zero_copy_kernel": ([vp, vp, c.c_uint32, vp, vp, vp, vp], c.c_int),
+        "vx_tuning_zero_copy_kernel": ([vp, vp, c.c_uint32, vp, vp, vp, c.c_int, vp], c.c_int),
         "vx_tuning_fail_submit_after": ([vp, c.c_int64], None),
         "vx_tuning_fail_launch_after": ([vp, c.c_int64], None),
         "vx_tuning_last_verify": ([vp, c.POINTER(vx_verify_trace)], c.c_int),
@@ -168,7 +173,7 @@ def lib() -> ctypes.CDLL:
                     "`python -c 'import __graft_entry__ as g; g.build()'` (or `make -C vortex_amd/csrc`).")
             L = ctypes.CDLL(LIB_PATH)
             _declare(L)
-            if L.vx_abi_version() != 1:
+            if L.vx_abi_version() != ABI_VERSION:
                 raise ImportError("libvortex_amd.so ABI version mismatch")
             _lib = L
     return _lib

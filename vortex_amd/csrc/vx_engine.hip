@@ -140,48 +140,22 @@ struct Slot {
 }  // namespace
 
 struct vx_ctx {
+    // Everything a caller chooses comes in here (vx_config, ABI 2): the
+    // engine reads no environment variables.
     vx_config cfg{};
     std::vector<Slot> slots;
     // H2D copies are serialised across slots in launch order, so PCIe moves
     // one batch at a time at full rate and batch k's kernel starts as soon as
-    // its own bytes are in, while batch k+1 copies.  (Copies racing on all
-    // slot streams share PCIe and delay every kernel.)  How the order is
-    // enforced is h2d_mode (VX_H2D_MODE, read at vx_create; see chain_h2d).
+    // its own bytes are in, while batch k+1 copies (chain_h2d).  (Copies
+    // racing on all slot streams share PCIe and delay every kernel.)
     int last_launched = -1;  // slot whose H2D was enqueued last
-    int prev_launched = -1;  // the one before it
-    int h2d_mode = 2;
-    // Chunk bytes for strided host batches of long pieces (§6.4); 0 = off.
-    uint64_t batch_chunk = 64 * 1024;
-    // Chunk bytes of the file re-verify (§6.3; 0 = chosen per call by
-    // verify_chunk_for), whether its first and last rounds ramp down to C/4,
-    // and the piece length above which it chunks (0 = pieces >= 2 chunks).
-    // Env overrides: VX_VERIFY_CHUNK, VX_VERIFY_RAMP, VX_VERIFY_CHUNKED_ABOVE.
-    uint64_t verify_chunk = 0;
-    // Chunk bytes when the torrent's data is not in the page cache
-    // (DirectIo::resident_fraction < 0.5 at the call's start), where the
-    // readers go O_DIRECT and the disk binds; warm calls keep
-    // verify_chunk_for's choice.  Off by default (VX_VERIFY_COLD_CHUNK=N
-    // turns it on): 1 MiB cold chunks measured +57 % and +7 % on two boxes
-    // but -2 % and -5 % (median of 6 and 10 evicted calls) on two more, 512
-    // KiB +4 % (profiles/r03/cold/ab_chunk_box*.jsonl, ab_cold_chunk_box*.jsonl):
-    // the box's disk decides, not the chunk.
-    uint64_t verify_cold_chunk = 0;
-    int verify_ramp = 1;  // ramp depth d: first/last rounds C / 2^(d+1) (0 = off)
-    int verify_ramp_growth = 0;  // head ramp: 0 = rounds double, 1 = grow x5/4 (VX_VERIFY_RAMP_GROWTH)
-    uint64_t verify_chunked_above = 0;
-    bool verify_overlap = true;  // read round k+1 while round k is enqueued (VX_VERIFY_OVERLAP)
-    uint32_t verify_readahead = 2;  // re-verify: rounds / slots read ahead of the enqueue (VX_VERIFY_READAHEAD)
-    bool verify_coalesce = true;    // whole-piece re-verify: one pread per run of pieces in one file (VX_VERIFY_COALESCE)
-    // re-verify reads of ranges not in the page cache go O_DIRECT (vx_files::DirectIo;
-    // VX_VERIFY_DIRECT: 0 = never, 1 = when not cached (default), 2 = whenever aligned)
-    int verify_direct = 1;
-    // re-verify reader threads pinned to the CPUs of the GPU's NUMA node
-    // (gpu_numa_cpus; VX_VERIFY_NUMA=1).  Off by default: on the shared GPU
-    // hosts it was +5 % / -1 % / +2 % / -10 % across four boxes
-    int verify_numa = 0;
-    // re-verify: extra reader threads that read O_DIRECT even when the data is
-    // cached (vx_files::Readers helpers; VX_VERIFY_HELPERS=N)
-    int verify_helpers = 0;
+    // cfg.verify_cold_chunk, when set, is used for calls whose data is not in
+    // the page cache (DirectIo::resident_fraction < 0.5 at the call's start),
+    // where the readers go O_DIRECT and the disk binds; warm calls keep
+    // verify_chunk_for's choice.  Off by default: 1 MiB cold chunks measured
+    // +57 % and +7 % on two boxes but -2 % and -5 % (median of 6 and 10
+    // evicted calls) on two more, 512 KiB +4 % (profiles/r03/cold/): the
+    // box's disk decides, not the chunk.
     uint64_t chunk_rounds = 0;  // chunk rounds launched (vx_tuning_chunk_rounds)
     // Per-piece device rows of the chunk paths (state | expected | digest |
     // verdict), kept across calls and grown on demand: allocating them per
@@ -189,7 +163,6 @@ struct vx_ctx {
     uint8_t* d_chunk_rows = nullptr;
     uint64_t chunk_rows_cap = 0;
     hipEvent_t chunk_prev = nullptr;
-    hipStream_t copy_stream = nullptr;  // mode 3 only
     // Device-resident `pieces` table (vx_set_piece_table).
     uint8_t* d_table = nullptr;
     uint32_t n_table = 0;
@@ -197,9 +170,7 @@ struct vx_ctx {
     // vx_flush found every other slot in flight and left the filling slot
     // open; vx_poll launches it once a slot frees.
     bool flush_pending = false;
-    bool lazy_flush = true;  // VX_LAZY_FLUSH=0: flush always launches (A/B)
-    bool batch_sort = true;  // VX_BATCH_SORT=0: host batches in caller order, batch_pieces launches (A/B)
-    bool bulk = false;       // inside vx_*_batch: slots fill to capacity, not to batch_pieces
+    bool bulk = false;  // inside vx_*_batch: slots fill to capacity, not to batch_pieces
     std::deque<vx_completion> done;
     struct Reg {
         size_t len;
@@ -211,17 +182,11 @@ struct vx_ctx {
     // one hash probe instead of a tree walk.  16 KiB pieces from 1,024
     // separately registered buffers: 29.7 -> 35.7 GiB/s.
     std::unordered_map<uintptr_t, Reg> registered_at;
-    bool gather = true;        // VX_GATHER=0 turns the gather kernel off (A/B)
-    // A slot whose pieces are all registered and aligned may be hashed
-    // straight out of host memory by the zero-copy kernel, without a gather
-    // (sha1_zc_split_kernel).  VX_ZERO_COPY=0 turns it off
-    // (A/B); any other value, and the default, takes every eligible slot.
-    bool zero_copy = true;
-    // The zero-copy kernel's form (zc_loader_wins): VX_ZC_LOADER 0 = the
-    // pair, 1 = with a loader wave, 2 = by the slot's piece count (default).
-    int zc_loader = 2;
-    uint64_t zero_copy_slots = 0;  // slots hashed that way (vx_tuning_zero_copy_slots)
-    uint32_t gather_grid = 0;  // VX_GATHER_GRID: workgroups per gather launch (0 = default)
+    // A slot whose pieces are all registered and aligned is hashed straight
+    // out of host memory by the zero-copy kernel, without a gather
+    // (sha1_zc_split_kernel), unless cfg.zero_copy is 0.
+    uint64_t zero_copy_slots = 0;         // slots hashed that way (vx_tuning_zero_copy_slots)
+    uint64_t zero_copy_loader_slots = 0;  // ... of them in the three-wave form (zc_loader_wins)
     uint64_t gather_tiles = 0;  // tiles gathered (vx_tuning_gather_tiles)
     uint64_t pending = 0;
     uint64_t seq = 0;
@@ -418,35 +383,21 @@ void stage_copies(Slot& s) {
 }
 
 // Order slot si's H2D after the previously launched slot's (one PCIe stream
-// of copies across all slots).  Modes:
-//   0  the slot stream waits on the previous slot's `copied` event;
-//   1  as 0, and the host first waits for the copy two launches back;
-//   2  the host waits for the previous slot's copy, no cross-stream wait
-//      (default);
-//   3  every H2D on one dedicated copy stream.
-// With 0 and 1, hipMemcpyAsync enqueued behind a cross-stream wait blocked
-// the host for ~8-9 ms at a time early in a run and left PCIe idle
-// (profiles/r01/e2e_first_use/).  A/B on one MI355X, 8192 x 256 KiB through
-// vx_verify_batch: 34-46 / 38-40 / 48.5-48.7 / 45 GiB/s for modes 0-3
-// (profiles/r01/h2d_modes/).  Mode 2 keeps copies back to back with a gap of
-// one host wake-up, and blocks the host for at most one batch's copy.
+// of copies across all slots): the host waits for the previous slot's copy,
+// with no cross-stream wait.  That keeps copies back to back with a gap of
+// one host wake-up and blocks the host for at most one batch's copy.  The
+// alternatives measured worse and were removed in round 4 (EXPERIMENTS.md):
+// a stream wait on the previous `copied` event blocked hipMemcpyAsync for
+// ~8-9 ms at a time and left PCIe idle (34-46 GiB/s, 38-40 with an extra
+// host wait two launches back), one dedicated copy stream 45, this 48.5-48.7
+// (8192 x 256 KiB through vx_verify_batch, profiles/r01/h2d_modes/).
 int chain_h2d(vx_ctx* c, int si) {
-    const int last = c->last_launched, prev = c->prev_launched;
-    const int mode = c->h2d_mode;
-    if (mode == 3) return 0;
-    if (mode == 1 && prev >= 0 && prev != si && prev != last) VX_HIP(hipEventSynchronize(c->slots[prev].copied));
-    if (mode == 2) {
-        if (last >= 0 && last != si) VX_HIP(hipEventSynchronize(c->slots[last].copied));
-        return 0;
-    }
-    if (last >= 0 && last != si) VX_HIP(hipStreamWaitEvent(c->slots[si].stream, c->slots[last].copied, 0));
+    const int last = c->last_launched;
+    if (last >= 0 && last != si) VX_HIP(hipEventSynchronize(c->slots[last].copied));
     return 0;
 }
 
-void mark_launched(vx_ctx* c, int si) {
-    if (c->last_launched != si) c->prev_launched = c->last_launched;
-    c->last_launched = si;
-}
+void mark_launched(vx_ctx* c, int si) { c->last_launched = si; }
 
 // Run every command type a batch uses once on every slot stream, in the
 // launch pattern of launch_slot_impl (cross-slot copy chain, large and small
@@ -483,7 +434,6 @@ int warm_slots(vx_ctx* c) {
     }
     for (auto& s : c->slots) VX_HIP(hipStreamSynchronize(s.stream));
     c->last_launched = prev;
-    c->prev_launched = -1;
     return 0;
 }
 
@@ -523,10 +473,11 @@ int launch_slot_impl(vx_ctx* c, int si) {
         s.state = Slot::FREE;
         return 0;
     }
-    hipStream_t cs = c->h2d_mode == 3 ? c->copy_stream : s.stream;
+    hipStream_t cs = s.stream;
     // Zero-copy slot: every piece is read by the hash kernel itself, so no
     // bytes cross PCIe ahead of it and nothing waits for the copy chain.
-    const bool zc = s.gtiles && s.all_mapped && c->zero_copy;
+    // Any slot qualifies, async or inside a host batch (vx_hash.h).
+    const bool zc = s.gtiles && s.all_mapped && c->cfg.zero_copy;
     stage_copies(s);
     if (!zc)
         if (int rc = chain_h2d(c, si)) return rc;
@@ -549,8 +500,8 @@ int launch_slot_impl(vx_ctx* c, int si) {
         // chain-bound pairs that barely touch HBM, so the gather may use 128
         // workgroups: async 2 / 4 MiB pieces 39.8 -> 43.2 / 35.8 -> 39.6 GiB/s.
         // With shorter pieces the hash kernels compete and 128 cost up to 10 %
-        // (1 MiB: -2 %).  VX_GATHER_GRID overrides.
-        const uint32_t grid = c->gather_grid ? c->gather_grid : (s.bytes >= (uint64_t)n << 21 ? 128u : 0u);
+        // (1 MiB: -2 %).
+        const uint32_t grid = s.bytes >= (uint64_t)n << 21 ? 128u : 0u;
         hipError_t e = vx::launch_gather(s.d_src, s.d_offsets, s.d_lens, s.d_tfirst, n, s.gtiles, s.d_arena, cs, grid);
         if (e != hipSuccess) return hip_fail(e, "gather launch");
         c->gather_tiles += s.gtiles;
@@ -563,13 +514,13 @@ int launch_slot_impl(vx_ctx* c, int si) {
     const uint8_t* d_exp = s.use_table ? c->d_table : (s.has_expected ? s.d_expected : nullptr);
     const uint32_t* d_row = s.use_table ? s.d_pidx : nullptr;
     VX_HIP(hipEventRecord(s.copied, cs));
-    if (cs != s.stream) VX_HIP(hipStreamWaitEvent(s.stream, s.copied, 0));
     mark_launched(c, si);
     hipError_t e;
     if (zc) {
-        const bool loader = c->zc_loader == 1 || (c->zc_loader == 2 && zc_loader_wins(n));
+        const bool loader = zc_loader_wins(n);
         e = vx::launch_zero_copy(s.d_src, s.d_lens, n, s.d_digests, d_exp, s.d_matched, loader, s.stream, d_row);
         c->zero_copy_slots++;
+        c->zero_copy_loader_slots += loader;
     } else if (s.uniform) {
         const uint32_t len = s.h_lens[0];
         const uint64_t stride = align_up(std::max<uint32_t>(len, 1), kAlign);
@@ -705,13 +656,15 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
     const uint8_t* dev = nullptr;
     s->h_src[i] = 0;
     if (i == 0) s->t_open = std::chrono::steady_clock::now();
-    if (len && c->gather && (reinterpret_cast<uintptr_t>(data) & 15) == 0 && is_registered(c, data, len, &dev)) {
+    if (len && (reinterpret_cast<uintptr_t>(data) & 15) == 0 && is_registered(c, data, len, &dev)) {
         // Registered, 16-byte aligned: the launch's gather kernel pulls it
         // through the range's device mapping.
         s->h_src[i] = reinterpret_cast<uint64_t>(dev);
         s->gtiles += vx::gather_tiles(len);
     } else if (len) {
-        s->all_mapped = false;
+        // all_mapped is cleared below, once the piece is certainly queued: a
+        // refused piece (VX_ENOMEM from ensure_stage) must not take the rest
+        // of the slot off the zero-copy path.
         if (is_registered(c, data, len)) {
             // Pinned source: DMA straight from the caller's buffer at launch;
             // pieces adjacent in host memory AND in the arena share one copy.
@@ -736,6 +689,7 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
             else
                 s->runs.push_back(Run{off, off + len});
         }
+        s->all_mapped = false;
     }
     s->h_offsets[i] = off;
     s->h_lens[i] = len;
@@ -822,6 +776,12 @@ void vx_config_default(vx_config* cfg, uint32_t max_piece_len) {
     const uint64_t piece = align_up(std::max<uint32_t>(max_piece_len, 1), kAlign);
     cfg->slot_bytes = std::max(piece, std::min<uint64_t>(2ull << 30, std::max<uint64_t>(128ull << 20, piece * 512)));
     cfg->batch_pieces = (uint32_t)std::min<uint64_t>(65536, cfg->slot_bytes / align_up(std::max<uint32_t>(max_piece_len, 1), kAlign));
+    cfg->zero_copy = 1;
+    cfg->direct_io = 1;
+    cfg->batch_chunk = 64 * 1024;
+    cfg->verify_chunk = 0;         // per call: verify_chunk_for
+    cfg->verify_cold_chunk = 0;
+    cfg->verify_ramp = 1;
 }
 
 int vx_create(const vx_config* cfg, vx_ctx** out) {
@@ -830,37 +790,19 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (cfg->max_piece_len == 0 || cfg->slots == 0 || cfg->batch_pieces == 0)
         return fail(VX_EINVAL, "vx_create: max_piece_len, slots and batch_pieces must be > 0");
     if (cfg->slot_bytes < cfg->max_piece_len) return fail(VX_EINVAL, "vx_create: slot_bytes < max_piece_len");
+    if (cfg->zero_copy > 1 || cfg->direct_io > 1)
+        return fail(VX_EINVAL, "vx_create: zero_copy and direct_io are 0 or 1");
+    if (cfg->verify_ramp > 5) return fail(VX_EINVAL, "vx_create: verify_ramp must be 0..5");
+    if ((cfg->batch_chunk && (cfg->batch_chunk < 4096 || cfg->batch_chunk % 4096)) ||
+        (cfg->verify_chunk && (cfg->verify_chunk < 4096 || cfg->verify_chunk % 4096)) ||
+        (cfg->verify_cold_chunk && (cfg->verify_cold_chunk < 4096 || cfg->verify_cold_chunk % 4096)))
+        return fail(VX_EINVAL, "vx_create: chunk sizes must be 0 or multiples of 4096");
     const int ndev = vx_device_count();
     if (cfg->device < 0 || cfg->device >= ndev) return fail(VX_ENODEV, "vx_create: no such HIP device");
     vx_ctx* c = new (std::nothrow) vx_ctx();
     if (!c) return fail(VX_ENOMEM, "vx_create: out of host memory");
     c->cfg = *cfg;
-    if (const char* m = std::getenv("VX_H2D_MODE")) c->h2d_mode = std::atoi(m) & 3;
-    if (const char* m = std::getenv("VX_GATHER")) c->gather = std::atoi(m) != 0;
-    if (const char* m = std::getenv("VX_GATHER_GRID")) c->gather_grid = (uint32_t)std::atoi(m);
-    if (const char* m = std::getenv("VX_ZERO_COPY")) c->zero_copy = std::atoi(m) != 0;
-    if (const char* m = std::getenv("VX_ZC_LOADER")) c->zc_loader = std::max(0, std::min(2, std::atoi(m)));
-    if (const char* m = std::getenv("VX_LAZY_FLUSH")) c->lazy_flush = std::atoi(m) != 0;
-    if (const char* m = std::getenv("VX_BATCH_SORT")) c->batch_sort = std::atoi(m) != 0;
-    if (const char* m = std::getenv("VX_BATCH_CHUNK")) c->batch_chunk = align_up(std::strtoull(m, nullptr, 0), kAlign);
-    if (const char* m = std::getenv("VX_VERIFY_CHUNK"))
-        c->verify_chunk = std::max<uint64_t>(4096, align_up(std::strtoull(m, nullptr, 0), 4096));
-    if (const char* m = std::getenv("VX_VERIFY_RAMP")) c->verify_ramp = std::max(0, std::min(5, std::atoi(m)));
-    if (const char* m = std::getenv("VX_VERIFY_RAMP_GROWTH")) c->verify_ramp_growth = std::atoi(m) != 0;
-    if (const char* m = std::getenv("VX_VERIFY_CHUNKED_ABOVE")) c->verify_chunked_above = std::strtoull(m, nullptr, 0);
-    if (const char* m = std::getenv("VX_VERIFY_OVERLAP")) c->verify_overlap = std::atoi(m) != 0;
-    if (const char* m = std::getenv("VX_VERIFY_COALESCE")) c->verify_coalesce = std::atoi(m) != 0;
-    if (const char* m = std::getenv("VX_VERIFY_READAHEAD")) c->verify_readahead = (uint32_t)std::max(1, std::atoi(m));
-    if (const char* m = std::getenv("VX_VERIFY_COLD_CHUNK")) {
-        const uint64_t v = std::strtoull(m, nullptr, 0);
-        c->verify_cold_chunk = v ? std::max<uint64_t>(4096, align_up(v, 4096)) : 0;
-    }
-    if (const char* m = std::getenv("VX_VERIFY_DIRECT")) c->verify_direct = std::max(0, std::min(3, std::atoi(m)));
-    if (const char* m = std::getenv("VX_VERIFY_NUMA")) c->verify_numa = std::atoi(m) != 0;
-    if (const char* m = std::getenv("VX_VERIFY_HELPERS")) c->verify_helpers = std::max(0, std::min(16, std::atoi(m)));
     int rc = set_device(c);
-    if (!rc && c->h2d_mode == 3 && hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess)
-        rc = fail(VX_EDEVICE, "vx_create: copy stream");
     if (!rc) {
         c->slots.resize(cfg->slots);
         for (auto& s : c->slots) {
@@ -871,7 +813,6 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (!rc) rc = warm_slots(c);
     if (rc) {
         for (auto& s : c->slots) free_slot_mem(s);
-        if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
         delete c;
         return rc;
     }
@@ -889,10 +830,8 @@ int vx_destroy(vx_ctx* c) {
     // return in-flight buffers to its pool as soon as this call returns.
     for (auto& s : c->slots)
         if (s.stream) (void)hipStreamSynchronize(s.stream);
-    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     for (auto& r : c->registered) (void)hipHostUnregister(reinterpret_cast<void*>(r.first));
     for (auto& s : c->slots) free_slot_mem(s);
-    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->d_table) (void)hipFree(c->d_table);
     if (c->d_chunk_rows) (void)hipFree(c->d_chunk_rows);
     if (c->chunk_prev) (void)hipEventDestroy(c->chunk_prev);
@@ -979,12 +918,10 @@ int vx_flush(vx_ctx* c) {
     if (c->filling < 0 || c->slots[c->filling].n == 0) return 0;
     int rc = set_device(c);
     if (rc) return rc;
-    if (c->lazy_flush) {
-        if ((rc = reap(c, false))) return rc;
-        if (!may_launch_now(c)) {
-            c->flush_pending = true;
-            return 0;
-        }
+    if ((rc = reap(c, false))) return rc;
+    if (!may_launch_now(c)) {
+        c->flush_pending = true;
+        return 0;
     }
     return launch_slot(c, c->filling);
 }
@@ -1085,49 +1022,6 @@ struct FileVerify {
     }
 };
 
-// The CPUs of the NUMA node the context's GPU hangs off (sysfs numa_node of
-// its PCI function, then that node's cpulist), intersected with this
-// process's affinity.  false when any step is unavailable or the
-// intersection is empty.
-bool gpu_numa_cpus(const vx_ctx* c, cpu_set_t* out) {
-    char bus[64] = {0};
-    if (hipDeviceGetPCIBusId(bus, sizeof(bus), c->cfg.device) != hipSuccess) return false;
-    for (char* p = bus; *p; ++p) *p = (char)std::tolower((unsigned char)*p);
-    auto read_line = [](const std::string& path) {
-        std::string v;
-        if (FILE* f = std::fopen(path.c_str(), "r")) {
-            char buf[4096];
-            if (std::fgets(buf, sizeof(buf), f)) v = buf;
-            std::fclose(f);
-        }
-        return v;
-    };
-    const std::string node = read_line(std::string("/sys/bus/pci/devices/") + bus + "/numa_node");
-    if (node.empty() || node[0] == '-') return false;
-    const std::string list = read_line("/sys/devices/system/node/node" + std::to_string(std::atoi(node.c_str())) +
-                                       "/cpulist");
-    cpu_set_t mine;
-    if (list.empty() || sched_getaffinity(0, sizeof(mine), &mine) != 0) return false;
-    CPU_ZERO(out);
-    size_t at = 0;
-    while (at < list.size()) {  // "0-63,128-191\n"
-        char* end = nullptr;
-        const long a = std::strtol(list.c_str() + at, &end, 10);
-        if (end == list.c_str() + at) break;
-        long b = a;
-        at = (size_t)(end - list.c_str());
-        if (at < list.size() && list[at] == '-') {
-            b = std::strtol(list.c_str() + at + 1, &end, 10);
-            at = (size_t)(end - list.c_str());
-        }
-        for (long k = a; k <= b && k < CPU_SETSIZE; ++k)
-            if (k >= 0 && CPU_ISSET(k, &mine)) CPU_SET(k, out);
-        if (at < list.size() && list[at] == ',') ++at;
-        else break;
-    }
-    return CPU_COUNT(out) > 0;
-}
-
 // Re-verify chunk size for `count` pieces: 256 KiB when
 // every piece's chunk fits one slot arena (a single window of rounds), else
 // 128 KiB.  A call split into windows ends on its last, smaller window, whose
@@ -1135,23 +1029,25 @@ bool gpu_numa_cpus(const vx_ctx* c, cpu_set_t* out) {
 // 1 MiB x 2,774 pieces 43.6 -> 46.8 GiB/s at 128 KiB, 256 KiB x 11,093 pieces
 // 37.5 (whole-piece slots) -> 45.0, 2 MiB x 1,387 best at 256 KiB + ramp.
 uint64_t verify_chunk_for(const vx_ctx* c, uint64_t count) {
-    if (c->verify_chunk) return c->verify_chunk;
+    if (c->cfg.verify_chunk) return c->cfg.verify_chunk;
     constexpr uint64_t big = 256 * 1024, small = 128 * 1024;
     return count * big <= c->slots[0].arena_cap && count <= c->slots[0].cap ? big : small;
 }
 
+// Re-verify reads run this many slots (whole pieces) or rounds (chunks)
+// ahead of the one being enqueued, bounded by the slots.
+constexpr size_t kReadahead = 2;
+
 // Both verify pieces [first, end) of an n-piece torrent; tags, bad[] and
-// matched_out are indexed from `first`.  Both queue reads up to
-// `verify_readahead` slots ahead of the slot being launched (see
-// verify_chunked).
+// matched_out are indexed from `first`.  Both queue reads up to kReadahead
+// slots ahead of the slot being launched (see verify_chunked).
 int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl, uint64_t total, uint64_t first,
                  uint64_t end) {
     vx_ctx* c = fv.c;
     const uint64_t stride = align_up(pl, kAlign);
     const uint64_t last_len = total - (n - 1) * (uint64_t)pl;
     const size_t nslots = c->slots.size();
-    const size_t depth =
-        c->verify_overlap && nslots > 1 ? std::min<size_t>(std::max<uint32_t>(1, c->verify_readahead), nslots - 1) : 0;
+    const size_t depth = nslots > 1 ? std::min<size_t>(kReadahead, nslots - 1) : 0;
     std::vector<std::vector<vx_files::ReadItem>> items(nslots);
     struct Queued {
         int si;
@@ -1159,17 +1055,17 @@ int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl,
     };
     std::deque<Queued> q;  // slots read or reading, in piece order, not yet launched
     // Runs of whole pieces inside one file go out as one pread of up to 4 MiB
-    // (vx_files::Runs; 16 KiB pieces were pread-bound); VX_VERIFY_COALESCE=0 reads piece by piece.
-    vx_files::Runs runs = rd.runs(c->verify_coalesce ? 4ull << 20 : 0);
+    // (vx_files::Runs; 16 KiB pieces were pread-bound).
+    vx_files::Runs runs = rd.runs(4ull << 20);
     // Ramps: nothing overlaps the first slot's read or the last slot's copy
     // and kernel, so the first slots take 1/2^L, ..., 1/4, 1/2 of a full
     // slot's pieces, the first one <= 64 MiB, and the last full slot's worth
-    // is split in halves down to that size (VX_VERIFY_RAMP=0 turns both off;
-    // as for chunks, §6.3).
+    // is split in halves down to that size (cfg.verify_ramp = 0 turns both
+    // off; as for chunks, §6.3).
     const uint64_t cap_full =
         std::min<uint64_t>(c->slots[0].cap, std::max<uint64_t>(1, c->slots[0].arena_cap / stride));
     int ramp = 0;
-    while (c->verify_ramp > 0 && ramp < 8 && (cap_full >> ramp) > 1 && (cap_full >> ramp) * stride > (64ull << 20))
+    while (c->cfg.verify_ramp > 0 && ramp < 8 && (cap_full >> ramp) > 1 && (cap_full >> ramp) * stride > (64ull << 20))
         ++ramp;
     int filled = 0;
     uint64_t next = first;
@@ -1404,8 +1300,7 @@ struct ChunkPipe {
 // of the pipeline nothing overlaps — shrink to q.  d = 1 is C/4, C/4, C/2.
 // Every boundary is a multiple of q (>= 64 bytes for C >= 4 KiB, d <= 5), so
 // no non-final chunk ends mid-block.
-std::vector<std::pair<uint64_t, uint64_t>> chunk_schedule(uint64_t L, uint64_t C, int head, int tail,
-                                                          bool gentle = false) {
+std::vector<std::pair<uint64_t, uint64_t>> chunk_schedule(uint64_t L, uint64_t C, int head, int tail) {
     std::vector<std::pair<uint64_t, uint64_t>> r;
     const int d = std::max(head, tail);
     const uint64_t q = C >> (d + 1);
@@ -1415,17 +1310,7 @@ std::vector<std::pair<uint64_t, uint64_t>> chunk_schedule(uint64_t L, uint64_t C
     if (ramp && head) {
         r.push_back({a, q});
         a += q;
-        if (gentle) {
-            // x5/4 per round, rounded up to u (4 KiB, or q when smaller): a round's
-            // read then fits under the previous round's copy, since the host reads
-            // ~1.3x faster than PCIe copies; doubling left the copy engine idle
-            // behind each larger read (profiles/r02/reverify_trace/)
-            const uint64_t u = std::min<uint64_t>(q, 4096);
-            for (uint64_t len = q; len < C; len = std::min(C, (len * 5 / 4 + u - 1) / u * u))
-                r.push_back({a, len}), a += len;
-        } else {
-            for (uint64_t len = q; len < C; len *= 2) r.push_back({a, len}), a += len;
-        }
+        for (uint64_t len = q; len < C; len *= 2) r.push_back({a, len}), a += len;
     }
     // the tail ramp covers the last R bytes, R in (C - q, C]: C/2, ..., q, R - (C - q)
     const uint64_t tail_from = ramp && tail ? (L - C + q - 1) / q * q : L;
@@ -1444,13 +1329,12 @@ std::vector<std::pair<uint64_t, uint64_t>> chunk_schedule(uint64_t L, uint64_t C
 
 // The rounds of every window, in order, each read into its own slot by the
 // reader pool and then enqueued (H2D + chunk kernel).  Reads run up to
-// `verify_readahead` rounds ahead of the round being enqueued (bounded by the
-// slots), queued on the pool so the readers never wait for an enqueue: with
-// one round of read-ahead the reads and the copy chain were coupled round by
-// round, and every round whose read outlasted the previous copy left PCIe
-// idle (the head ramp's doubling rounds most of all).
-// VX_TRACE_ROUNDS=1 prints per-round host timings and, after the call, each
-// round's data copy as the GPU timed it.
+// kReadahead rounds ahead of the round being enqueued (bounded by the slots),
+// queued on the pool so the readers never wait for an enqueue: with one round
+// of read-ahead the reads and the copy chain were coupled round by round, and
+// every round whose read outlasted the previous copy left PCIe idle (the head
+// ramp's doubling rounds most of all).  Each round's data
+// copy is timed on the GPU (vx_tuning_last_verify).
 int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl, uint64_t total, uint64_t first,
                    uint64_t end, uint64_t C) {
     vx_ctx* c = fv.c;
@@ -1473,26 +1357,20 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     for (uint64_t w0 = first; w0 < end; w0 += W) {
         const uint64_t w1 = std::min<uint64_t>(end, w0 + W);
         const uint64_t wmax = w1 == n ? std::max<uint64_t>(pl, last_len) : pl;
-        const auto sched = chunk_schedule(wmax, C, w0 == first ? c->verify_ramp : 0, w1 == end ? c->verify_ramp : 0,
-                                          c->verify_ramp_growth != 0);
+        const int ramp = (int)c->cfg.verify_ramp;
+        const auto sched = chunk_schedule(wmax, C, w0 == first ? ramp : 0, w1 == end ? ramp : 0);
         for (size_t k = 0; k < sched.size(); ++k)
             rounds.push_back(Round{w0, w1, sched[k].first, sched[k].second, k > 0, -1, 0, 0, 0});
     }
     const size_t nslots = c->slots.size();
-    const size_t depth =
-        c->verify_overlap && nslots > 1 ? std::min<size_t>(std::max<uint32_t>(1, c->verify_readahead), nslots - 1) : 0;
+    const size_t depth = nslots > 1 ? std::min<size_t>(kReadahead, nslots - 1) : 0;
     std::vector<std::vector<vx_files::ReadItem>> items(nslots);
-    static const bool trace = [] {
-        const char* e = std::getenv("VX_TRACE_ROUNDS");
-        return e && e[0] == '1';
-    }();
     using clk = std::chrono::steady_clock;
-    const auto t_call = clk::now();
     auto ms = [](clk::time_point a, clk::time_point b) {
         return std::chrono::duration<double, std::milli>(b - a).count();
     };
     // A (start, end) timing-event pair around each round's data copy, kept on
-    // the context and reused (vx_tuning_last_verify; VX_TRACE_ROUNDS prints them).
+    // the context and reused (vx_tuning_last_verify).
     size_t timed = 0;
     std::vector<uint64_t> timed_bytes;
     auto t_last_enqueue = clk::now();
@@ -1538,14 +1416,11 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     };
     size_t nr = 0;  // next round to read
     for (size_t ne = 0; ne < rounds.size() && !rc; ++ne) {
-        const auto t_a = clk::now();
         while (nr < rounds.size() && nr <= ne + depth && start_read(rounds[nr], nr == ne)) ++nr;
         if (rc) break;
         Round& r = rounds[ne];
         if (r.m == 0) continue;
-        const auto t_b = clk::now();
         rd.wait(r.ticket);
-        const auto t_c = clk::now();
         rc = cp.round(r.si, r.m, r.continues, false, [&](Slot& sl, hipStream_t st) {
             bool ev = true;
             while (ev && c->copy_ev.size() < 2 * timed + 2) {
@@ -1563,10 +1438,6 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
             return 0;
         });
         t_last_enqueue = clk::now();
-        if (trace)
-            std::fprintf(stderr,
-                         "vx round %zu slot %d at %.2f: slots+reads %.2f read wait %.2f enqueue %.2f (%zu reading)\n",
-                         ne, r.si, ms(t_call, t_a), ms(t_a, t_b), ms(t_b, t_c), ms(t_c, clk::now()), nr - ne - 1);
     }
     rd.wait();  // error path: no read may still target a stage
     for (auto& sl : c->slots)  // rounds read but never launched (error path)
@@ -1578,16 +1449,12 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     vx_verify_trace& vt = c->last_verify;
     vt.tail_ms = ms(t_last_enqueue, clk::now());
     if (!rc && timed) {  // finish() waited for every round: the copy events are complete
-        float t0 = 0, a = 0, b = 0, busy = 0;
+        float a = 0, b = 0, busy = 0;
         for (size_t k = 0; k < timed; ++k) {
             (void)hipEventElapsedTime(&a, c->copy_ev[0], c->copy_ev[2 * k]);
             (void)hipEventElapsedTime(&b, c->copy_ev[0], c->copy_ev[2 * k + 1]);
             busy += b - a;
             vt.copy_bytes += timed_bytes[k];
-            if (trace)
-                std::fprintf(stderr, "vx copy %zu: %.3f -> %.3f ms (%.3f ms, ~%.1f GiB/s) gap %.3f\n", k, a, b,
-                             b - a, timed_bytes[k] / ((b - a) * 1e-3) / (1 << 30), a - t0);
-            t0 = b;
         }
         vt.copy_busy_ms = busy;
         vt.copy_span_ms = b;
@@ -1611,7 +1478,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
 // chain trails it, instead of a whole-piece chain per slot.
 bool strided_batch(const vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, size_t n,
                    uint64_t* host_stride) {
-    const uint64_t C = c->batch_chunk;
+    const uint64_t C = c->cfg.batch_chunk;
     if (n == 0 || C == 0 || c->slots[0].arena_cap < C) return false;
     const uint32_t L = lens[0];
     if (L < 2 * C || L > c->cfg.max_piece_len || lens[n - 1] == 0 || lens[n - 1] > L) return false;
@@ -1628,7 +1495,7 @@ bool strided_batch(const vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* 
 
 int batch_chunked(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, const uint8_t* expected, size_t n,
                   uint8_t* matched_out, uint8_t* digests_out, uint64_t hs) {
-    const uint64_t C = c->batch_chunk;
+    const uint64_t C = c->cfg.batch_chunk;
     const uint64_t L = lens[0], Llast = lens[n - 1];
     const uint8_t* base = ptrs[0];
     ChunkPipe cp(c);
@@ -1685,8 +1552,8 @@ int batch_chunked(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, c
 // reads bytes [a, a + C) of its piece.
 bool gather_batch(const vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens, size_t n,
                   std::vector<const uint8_t*>& dev) {
-    const uint64_t C = c->batch_chunk;
-    if (n == 0 || !c->gather || C == 0 || c->slots[0].arena_cap < C) return false;
+    const uint64_t C = c->cfg.batch_chunk;
+    if (n == 0 || C == 0 || c->slots[0].arena_cap < C) return false;
     uint32_t max_len = 0;
     dev.assign(n, nullptr);
     for (size_t i = 0; i < n; ++i) {
@@ -1701,121 +1568,79 @@ bool gather_batch(const vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* l
 
 int batch_chunked_gather(vx_ctx* c, const uint32_t* lens, const uint8_t* expected, size_t n, uint8_t* matched_out,
                          uint8_t* digests_out, const std::vector<const uint8_t*>& dev) {
-    const uint64_t C = c->batch_chunk;
+    const uint64_t C = c->cfg.batch_chunk;
     ChunkPipe cp(c);
     int rc = cp.open(n, expected, "batch");
     for (size_t i = 0; i < n; ++i) cp.bytes += lens[i];
     const Slot& s0 = c->slots[0];
     const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>(s0.cap, s0.arena_cap / C));
-    // Windows take the pieces longest first (stable, so equal lengths keep the
-    // caller's order).  Every round of a window is one C-byte chain whatever
-    // its lane count, and a window runs rounds up to its longest piece: with a
-    // few long pieces in every window, every window pays that whole chain
-    // while its late rounds carry a few MiB each.  Grouped, the long pieces
-    // share rounds that stay PCIe-bound and the short ones finish in one
-    // round (config 3 from host: DESIGN.md §6.4).
+    // Pieces go longest first (stable, so equal lengths keep the caller's
+    // order).  Every round is one C-byte chain whatever its lane count; in
+    // caller-order windows every window with a long piece paid that whole
+    // chain while its late rounds carried a few MiB each (config 3 from host,
+    // DESIGN.md §6.4; that variant was removed in round 4, EXPERIMENTS.md).
     std::vector<uint32_t> order(n);
     std::iota(order.begin(), order.end(), 0u);
-    if (c->batch_sort)
-        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return lens[x] > lens[y]; });
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return lens[x] > lens[y]; });
     auto gather_copy = [&](uint32_t m, uint32_t tiles) {
         return [&, m, tiles](Slot& sl, hipStream_t st) -> int {
             if (hipMemcpyAsync(sl.d_src, sl.h_src, (size_t)m * 8, hipMemcpyHostToDevice, st) != hipSuccess ||
                 hipMemcpyAsync(sl.d_tfirst, sl.h_tfirst, (size_t)(m + 1) * 4, hipMemcpyHostToDevice, st) !=
                     hipSuccess)
                 return fail(VX_EDEVICE, "batch: gather table H2D failed");
-            hipError_t e = vx::launch_gather(sl.d_src, sl.d_offsets, sl.d_lens, sl.d_tfirst, m, tiles, sl.d_arena, st,
-                                             c->gather_grid);
+            hipError_t e = vx::launch_gather(sl.d_src, sl.d_offsets, sl.d_lens, sl.d_tfirst, m, tiles, sl.d_arena, st);
             if (e != hipSuccess) return hip_fail(e, "batch: gather launch");
             c->gather_tiles += tiles;
             c->stats.gather_tiles += tiles;
             return 0;
         };
     };
-    if (c->batch_sort) {
-        // Streaming rounds: a piece takes a lane from its first chunk to its
-        // last, and new pieces (longest first) join any round until it holds
-        // `target` bytes.  So the short pieces ride along the long pieces'
-        // later rounds instead of queueing behind them, and no round is a
-        // C-byte chain that moves only a few MiB.
-        uint64_t total = 0;
-        for (size_t i = 0; i < n; ++i) total += lens[i];
-        const uint64_t max_rounds = std::max<uint64_t>(1, (n ? (uint64_t)lens[order[0]] + C - 1 : 0) / C);
-        // Spread evenly over the longest piece's rounds: a round is bound by
-        // max(its bytes over PCIe, one C-byte chain), and the batch cannot take
-        // fewer rounds than its longest piece has chunks.  (A uniform batch gets
-        // target = n*C: every piece in the first round, as a window would.)
-        const uint64_t target = std::max<uint64_t>(1, (total + max_rounds - 1) / max_rounds);
-        std::vector<std::pair<uint32_t, uint64_t>> act, keep;  // (piece, next offset)
-        size_t next = 0;
-        while (!rc && (!act.empty() || next < n)) {
-            const int si = cp.free_slot([] {});
-            if (si < 0) {
-                rc = si;
-                break;
-            }
-            Slot& s = c->slots[si];
-            reset_fill(s);
-            uint32_t m = 0, tiles = 0;
-            uint64_t bytes = 0;
-            keep.clear();
-            auto lane = [&](uint32_t i, uint64_t a) {
-                const uint64_t L = lens[i];
-                const uint32_t clen = (uint32_t)std::min<uint64_t>(C, L - a);
-                s.h_offsets[m] = (uint64_t)m * C;
-                s.h_lens[m] = clen;
-                s.h_pidx[m] = i;
-                s.h_poff[m] = a;
-                s.h_tlen[m] = L;
-                s.h_src[m] = clen ? reinterpret_cast<uint64_t>(dev[i] + a) : 0;
-                tiles += clen ? vx::gather_tiles(clen) : 0;
-                s.h_tfirst[m + 1] = tiles;
-                ++m;
-                bytes += clen;
-                if (a + clen < L) keep.emplace_back(i, a + clen);
-            };
-            const bool continues = !act.empty();
-            for (const auto& pa : act) lane(pa.first, pa.second);
-            while (next < n && m < W && (bytes < target || m == 0)) lane(order[next++], 0);
-            act.swap(keep);
-            rc = cp.round(si, m, continues, true, gather_copy(m, tiles));
+    // Streaming rounds: a piece takes a lane from its first chunk to its
+    // last, and new pieces (longest first) join any round until it holds
+    // `target` bytes.  So the short pieces ride along the long pieces'
+    // later rounds instead of queueing behind them, and no round is a
+    // C-byte chain that moves only a few MiB.
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; ++i) total += lens[i];
+    const uint64_t max_rounds = std::max<uint64_t>(1, (n ? (uint64_t)lens[order[0]] + C - 1 : 0) / C);
+    // Spread evenly over the longest piece's rounds: a round is bound by
+    // max(its bytes over PCIe, one C-byte chain), and the batch cannot take
+    // fewer rounds than its longest piece has chunks.  (A uniform batch gets
+    // target = n*C: every piece in the first round, as a window would.)
+    const uint64_t target = std::max<uint64_t>(1, (total + max_rounds - 1) / max_rounds);
+    std::vector<std::pair<uint32_t, uint64_t>> act, keep;  // (piece, next offset)
+    size_t next = 0;
+    while (!rc && (!act.empty() || next < n)) {
+        const int si = cp.free_slot([] {});
+        if (si < 0) {
+            rc = si;
+            break;
         }
-        return cp.finish(matched_out, digests_out, rc);
-    }
-    for (uint64_t w0 = 0; w0 < n && !rc; w0 += W) {
-        const uint64_t w1 = std::min<uint64_t>(n, w0 + W);
-        uint64_t wmax = 0;
-        for (uint64_t p = w0; p < w1; ++p) wmax = std::max<uint64_t>(wmax, lens[order[p]]);
-        const uint64_t rounds = std::max<uint64_t>(1, (wmax + C - 1) / C);
-        for (uint64_t k = 0; k < rounds && !rc; ++k) {
-            const uint64_t a = k * C;
-            const int si = cp.free_slot([] {});
-            if (si < 0) {
-                rc = si;
-                break;
-            }
-            Slot& s = c->slots[si];
-            reset_fill(s);
-            uint32_t m = 0, tiles = 0;
-            for (uint64_t p = w0; p < w1; ++p) {
-                const uint64_t i = order[p];
-                const uint64_t L = lens[i];
-                if (a >= L && !(a == 0 && L == 0)) continue;  // piece finished
-                const uint32_t clen = (uint32_t)std::min<uint64_t>(C, L - a);
-                s.h_offsets[m] = (uint64_t)m * C;
-                s.h_lens[m] = clen;
-                s.h_pidx[m] = (uint32_t)i;
-                s.h_poff[m] = a;
-                s.h_tlen[m] = L;
-                s.h_src[m] = clen ? reinterpret_cast<uint64_t>(dev[i] + a) : 0;
-                tiles += clen ? vx::gather_tiles(clen) : 0;
-                s.h_tfirst[m + 1] = tiles;
-                ++m;
-            }
-            if (m == 0) continue;
-            rc = cp.round(si, m, k > 0, true, gather_copy(m, tiles));
-        }
-        cp.end_window();
+        Slot& s = c->slots[si];
+        reset_fill(s);
+        uint32_t m = 0, tiles = 0;
+        uint64_t bytes = 0;
+        keep.clear();
+        auto lane = [&](uint32_t i, uint64_t a) {
+            const uint64_t L = lens[i];
+            const uint32_t clen = (uint32_t)std::min<uint64_t>(C, L - a);
+            s.h_offsets[m] = (uint64_t)m * C;
+            s.h_lens[m] = clen;
+            s.h_pidx[m] = i;
+            s.h_poff[m] = a;
+            s.h_tlen[m] = L;
+            s.h_src[m] = clen ? reinterpret_cast<uint64_t>(dev[i] + a) : 0;
+            tiles += clen ? vx::gather_tiles(clen) : 0;
+            s.h_tfirst[m + 1] = tiles;
+            ++m;
+            bytes += clen;
+            if (a + clen < L) keep.emplace_back(i, a + clen);
+        };
+        const bool continues = !act.empty();
+        for (const auto& pa : act) lane(pa.first, pa.second);
+        while (next < n && m < W && (bytes < target || m == 0)) lane(order[next++], 0);
+        act.swap(keep);
+        rc = cp.round(si, m, continues, true, gather_copy(m, tiles));
     }
     return cp.finish(matched_out, digests_out, rc);
 }
@@ -1894,9 +1719,8 @@ static int batch_impl(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* len
     }
     std::vector<uint32_t> order(n);
     std::iota(order.begin(), order.end(), 0u);
-    if (c->batch_sort)
-        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return lens[x] > lens[y]; });
-    c->bulk = c->batch_sort;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return lens[x] > lens[y]; });
+    c->bulk = true;
     for (size_t p = 0; p < n; ++p) {
         const size_t i = order[p];
         rc = submit_impl(c, i, ptrs[i], lens[i], expected ? expected + i * 20 : nullptr);
@@ -1939,7 +1763,7 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
         return fail(VX_EINVAL, "vx_verify_files: n_pieces does not match the files' total length");
     if (count == 0) return 0;
     const uint64_t C = verify_chunk_for(c, count);
-    bool chunked = c->verify_chunked_above ? piece_length > c->verify_chunked_above : piece_length >= 2 * C;
+    bool chunked = piece_length >= 2 * C;
     if (piece_length > c->cfg.max_piece_len) chunked = true;  // whole pieces would not fit a slot
     if (chunked ? c->slots[0].arena_cap < C : piece_length > c->cfg.max_piece_len)
         return fail(VX_ERANGE, "vx_verify_files: pieces do not fit the context's slots");
@@ -1956,16 +1780,13 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
     std::vector<uint8_t> bad(count, 0);
     std::memset(matched_out, 0, count);
     {
-        const vx_files::DirectIo dio(paths, fds, c->verify_direct);
-        cpu_set_t numa;
-        const bool pin = c->verify_numa && gpu_numa_cpus(c, &numa);
-        vx_files::Readers rd(nthreads, fs, fds, piece_length, bad.data(), first, &dio, pin ? &numa : nullptr,
-                             c->verify_direct ? c->verify_helpers : 0);
+        const vx_files::DirectIo dio(fds, c->cfg.direct_io != 0);
+        vx_files::Readers rd(nthreads, fs, fds, piece_length, bad.data(), first, &dio);
         FileVerify fv{c, expected, matched_out, bad};
         c->harvest_counts_mismatches = false;
         // Uncached data: the disk binds, and takes bigger reads better.
-        const uint64_t Cc = c->verify_cold_chunk;
-        const uint64_t Cv = chunked && !c->verify_chunk && c->verify_direct && Cc > C &&
+        const uint64_t Cc = c->cfg.verify_cold_chunk;
+        const uint64_t Cv = chunked && !c->cfg.verify_chunk && c->cfg.direct_io && Cc > C &&
                                     piece_length >= 2 * Cc && c->slots[0].arena_cap >= Cc &&
                                     dio.resident_fraction() < 0.5
                                 ? Cc
@@ -2194,6 +2015,7 @@ uint64_t vx_tuning_chunk_rounds(const vx_ctx* c) { return c ? c->chunk_rounds : 
 uint64_t vx_tuning_gather_tiles(const vx_ctx* c) { return c ? c->gather_tiles : 0; }
 
 uint64_t vx_tuning_zero_copy_slots(const vx_ctx* c) { return c ? c->zero_copy_slots : 0; }
+uint64_t vx_tuning_zero_copy_loader_slots(const vx_ctx* c) { return c ? c->zero_copy_loader_slots : 0; }
 
 int vx_tuning_zero_copy_plan(uint32_t n, uint64_t total_len) {
     (void)total_len;  // the policy no longer depends on the slot's bytes (kept in the signature)
@@ -2201,14 +2023,13 @@ int vx_tuning_zero_copy_plan(uint32_t n, uint64_t total_len) {
 }
 
 int vx_tuning_zero_copy_kernel(const uint64_t* d_srcs, const uint32_t* d_lens, uint32_t n, void* d_digests,
-                               const void* d_expected, void* d_matched, void* stream) {
+                               const void* d_expected, void* d_matched, int loader, void* stream) {
     if (n && (!d_srcs || !d_lens || !d_digests)) return fail(VX_EINVAL, "vx_tuning_zero_copy_kernel: NULL argument");
     if ((d_expected == nullptr) != (d_matched == nullptr))
         return fail(VX_EINVAL, "vx_tuning_zero_copy_kernel: expected and matched go together");
-    const char* l = std::getenv("VX_ZC_LOADER");  // 1: the three-wave form
     hipError_t e = vx::launch_zero_copy(d_srcs, d_lens, n, static_cast<uint8_t*>(d_digests),
                                         static_cast<const uint8_t*>(d_expected), static_cast<uint8_t*>(d_matched),
-                                        l && l[0] == '1', static_cast<hipStream_t>(stream));
+                                        loader != 0, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? 0 : hip_fail(e, "vx_tuning_zero_copy_kernel");
 }
 int vx_tuning_last_verify(const vx_ctx* c, vx_verify_trace* out) {

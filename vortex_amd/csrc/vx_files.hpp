@@ -13,11 +13,8 @@
 // into that slot's pinned stage while the GPU copies and hashes the slots
 // already launched; a piece's segments land back to back at its arena offset.
 #include <fcntl.h>
-#include <pthread.h>
-#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
-#include <sys/uio.h>
 #include <unistd.h>
 
 #include <cerrno>
@@ -129,7 +126,12 @@ struct ReadItem {
 // PROT_READ mapping of the file, which faults nothing in) and destination,
 // offset and length are 4 KiB aligned, the range goes through an O_DIRECT
 // descriptor; an unaligned tail, a cached range, or a direct read that fails
-// goes through the normal one.  Bytes are the file's either way.
+// goes through the normal one.  Bytes are the file's either way: the O_DIRECT
+// descriptor is a reopen of the caller's own descriptor (/proc/self/fd/N),
+// checked to be the same inode, so a path renamed or replaced after the
+// buffered open can never mix two files' bytes in one piece.
+// (Round 3 also tried O_DIRECT whenever aligned, and RWF_NOWAIT reads from the
+// page cache first: neither beat the mincore probe; removed in round 4.)
 class DirectIo {
   public:
     static constexpr uint64_t kBlock = 4096;  // covers 512 B and 4 KiB logical blocks
@@ -139,18 +141,22 @@ class DirectIo {
     // descriptors or mappings (vm.max_map_count) in the middle of a call.
     static constexpr uint64_t kMinFile = 1ull << 20;
     static constexpr size_t kMaxFiles = 4096;
-    // mode: 0 = off, 1 = when the range's first page is not cached (mincore),
-    // 2 = whenever aligned (A/B), 3 = read from the page cache without waiting
-    // (preadv2 RWF_NOWAIT) and O_DIRECT whatever it could not return (A/B)
-    DirectIo(const char* const* paths, const std::vector<int>& fds, int mode)
-        : mode_(mode), dfd_(fds.size(), -1), map_(fds.size(), nullptr), size_(fds.size(), 0) {
-        if (mode_ == 0) return;
+    // enabled = false: every read is buffered (vx_config.direct_io = 0).
+    DirectIo(const std::vector<int>& fds, bool enabled)
+        : dfd_(fds.size(), -1), map_(fds.size(), nullptr), size_(fds.size(), 0) {
+        if (!enabled) return;
         size_t used = 0;
         for (size_t f = 0; f < fds.size() && used < kMaxFiles; ++f) {
             struct stat st;
             if (fds[f] < 0 || fstat(fds[f], &st) != 0 || !S_ISREG(st.st_mode) || st.st_size < (off_t)kMinFile) continue;
-            const int d = open(paths[f], O_RDONLY | O_DIRECT | O_CLOEXEC);
+            const std::string self = "/proc/self/fd/" + std::to_string(fds[f]);
+            const int d = open(self.c_str(), O_RDONLY | O_DIRECT | O_CLOEXEC);
             if (d < 0) continue;  // the filesystem refuses O_DIRECT: buffered reads only
+            struct stat dst;
+            if (fstat(d, &dst) != 0 || dst.st_dev != st.st_dev || dst.st_ino != st.st_ino) {
+                close(d);
+                continue;
+            }
             void* m = mmap(nullptr, (size_t)st.st_size, PROT_READ, MAP_SHARED, fds[f], 0);
             if (m == MAP_FAILED) {
                 close(d);
@@ -172,38 +178,11 @@ class DirectIo {
     DirectIo& operator=(const DirectIo&) = delete;
 
     // Read [off, off+len) of file f into dst; buffered_fd is the normal descriptor.
-    // force: O_DIRECT whenever aligned, cached or not (the direct helpers).
-    bool read(uint32_t f, int buffered_fd, uint8_t* dst, int64_t off, int64_t len, bool force = false) const {
+    bool read(uint32_t f, int buffered_fd, uint8_t* dst, int64_t off, int64_t len) const {
         const bool aligned = f < dfd_.size() && dfd_[f] >= 0 && len >= (int64_t)kBlock && off >= 0 &&
                              ((reinterpret_cast<uintptr_t>(dst) | (uint64_t)off) & (kBlock - 1)) == 0 &&
                              (uint64_t)(off + len) <= size_[f];
-        if (aligned && mode_ == 3 && !force && !nowait_unsupported_.load(std::memory_order_relaxed)) {
-            // Whatever the page cache holds comes back at once; the read stops
-            // at the first page that would need the disk.
-            int64_t got = 0;
-            while (got < len) {
-                struct iovec v{dst + got, (size_t)(len - got)};
-                const ssize_t r = preadv2(buffered_fd, &v, 1, (off_t)(off + got), RWF_NOWAIT);
-                if (r > 0) {
-                    got += r;
-                    continue;
-                }
-                if (r < 0 && (errno == EOPNOTSUPP || errno == EINVAL))
-                    nowait_unsupported_.store(true, std::memory_order_relaxed);  // mincore from now on
-                break;
-            }
-            if (got == len) return true;
-            const int64_t o = off + got, n = len - got;  // the uncached rest
-            if (n >= (int64_t)kBlock && ((reinterpret_cast<uintptr_t>(dst + got) | (uint64_t)o) & (kBlock - 1)) == 0) {
-                const int64_t head = n & ~(int64_t)(kBlock - 1);
-                if (read_full(dfd_[f], dst + got, o, head)) {
-                    direct_bytes_.fetch_add((uint64_t)head, std::memory_order_relaxed);
-                    return head == n || read_full(buffered_fd, dst + got + head, o + head, n - head);
-                }
-            }
-            return read_full(buffered_fd, dst + got, o, n);
-        }
-        if (aligned && (mode_ == 2 || force || !resident(f, off))) {
+        if (aligned && !resident(f, off)) {
             const int64_t head = len & ~(int64_t)(kBlock - 1);
             if (read_full(dfd_[f], dst, off, head)) {
                 direct_bytes_.fetch_add((uint64_t)head, std::memory_order_relaxed);
@@ -241,8 +220,6 @@ class DirectIo {
         unsigned char v = 0;
         return mincore(static_cast<uint8_t*>(map_[f]) + off, 1, &v) != 0 || (v & 1);  // unknown: stay buffered
     }
-    const int mode_;
-    mutable std::atomic<bool> nowait_unsupported_{false};
     std::vector<int> dfd_;
     std::vector<void*> map_;
     std::vector<uint64_t> size_;
@@ -251,14 +228,14 @@ class DirectIo {
 
 // Bytes [start, start+len) of a piece, mapped onto its file segments.
 inline bool read_range(const std::vector<FileSpan>& fs, const std::vector<int>& fds, uint32_t piece_length,
-                       const ReadItem& it, std::vector<Seg>& segs, const DirectIo* dio = nullptr, bool force = false) {
+                       const ReadItem& it, std::vector<Seg>& segs, const DirectIo* dio = nullptr) {
     segments(fs, (int64_t)it.piece, piece_length, segs);
     int64_t pos = 0, at = 0;
     const int64_t a = (int64_t)it.start, b = (int64_t)(it.start + it.len);
     for (const Seg& s : segs) {
         const int64_t lo = std::max<int64_t>(a, pos), hi = std::min<int64_t>(b, pos + s.len);
         if (lo < hi) {
-            const bool ok = dio ? dio->read(s.file, fds[s.file], it.dst + at, s.off + (lo - pos), hi - lo, force)
+            const bool ok = dio ? dio->read(s.file, fds[s.file], it.dst + at, s.off + (lo - pos), hi - lo)
                                 : read_full(fds[s.file], it.dst + at, s.off + (lo - pos), hi - lo);
             if (!ok) return false;
             at += hi - lo;
@@ -328,39 +305,17 @@ class Runs {
 // is the first piece of the verified range.
 class Readers {
   public:
-    // cpus (may be NULL): pin every reader thread to this set (the GPU's NUMA
-    // node, vx_engine.hip gpu_numa_cpus); pinning is best effort.
-    // helpers: extra threads that read their items with O_DIRECT even when the
-    // data is cached (DirectIo force), so the drive's DMA adds to the CPU's
-    // page-cache copies on hosts where those copies are the limit; a helper
-    // whose direct read runs slower than kHelperMinRate stops for the call.
-    static constexpr double kHelperMinRate = 0.2e9;  // bytes per second of one request (QD1)
     Readers(int n, const std::vector<FileSpan>& fs, const std::vector<int>& fds, uint32_t piece_length,
-            uint8_t* bad, uint64_t first = 0, const DirectIo* dio = nullptr, const cpu_set_t* cpus = nullptr,
-            int helpers = 0)
+            uint8_t* bad, uint64_t first = 0, const DirectIo* dio = nullptr)
         : fs_(fs), fds_(fds), pl_(piece_length), bad_(bad), first_(first), dio_(dio) {
-        if (cpus) {
-            cpus_ = *cpus;
-            pin_ = true;
-        }
         for (int t = 0; t < n; ++t) {
             try {
-                th_.emplace_back([this] {
-                    if (pin_) (void)pthread_setaffinity_np(pthread_self(), sizeof(cpus_), &cpus_);
-                    loop();
-                });
+                th_.emplace_back([this] { loop(); });
             } catch (...) {  // no more threads: the ones already started do the reads
                 break;
             }
         }
         if (th_.empty()) inline_ = true;  // not even one: submit() reads on the caller's thread
-        for (int t = 0; t < helpers && dio_ && !inline_; ++t) {
-            try {
-                th_.emplace_back([this] { loop(true); });
-            } catch (...) {
-                break;
-            }
-        }
     }
     ~Readers() {
         {
@@ -430,11 +385,11 @@ class Readers {
     // wait(), which orders it through mu_.
     void mark_bad(uint64_t piece) { __atomic_store_n(&bad_[piece - first_], (uint8_t)1, __ATOMIC_RELAXED); }
     // Returns the item's read time in ns.
-    uint64_t read_item(const ReadItem& it, std::vector<Seg>& segs, bool force = false) {
+    uint64_t read_item(const ReadItem& it, std::vector<Seg>& segs) {
         const uint64_t t0 = now_ns();
         uint64_t expect = 0;
         first_ns_.compare_exchange_strong(expect, t0, std::memory_order_relaxed);
-        read_item_impl(it, segs, force);
+        read_item_impl(it, segs);
         const uint64_t t1 = now_ns();
         busy_ns_.fetch_add(t1 - t0, std::memory_order_relaxed);
         bytes_.fetch_add(it.len, std::memory_order_relaxed);
@@ -445,15 +400,14 @@ class Readers {
         }
         return t1 - t0;
     }
-    void read_item_impl(const ReadItem& it, std::vector<Seg>& segs, bool force) {
+    void read_item_impl(const ReadItem& it, std::vector<Seg>& segs) {
         if (it.file >= 0) {
-            const bool ok = dio_ ? dio_->read((uint32_t)it.file, fds_[it.file], it.dst, it.file_off, (int64_t)it.len,
-                                              force)
+            const bool ok = dio_ ? dio_->read((uint32_t)it.file, fds_[it.file], it.dst, it.file_off, (int64_t)it.len)
                                  : read_full(fds_[it.file], it.dst, it.file_off, (int64_t)it.len);
             if (ok) return;
         }
         if (it.file < 0) {
-            if (!read_range(fs_, fds_, pl_, it, segs, dio_, force)) mark_bad(it.piece);
+            if (!read_range(fs_, fds_, pl_, it, segs, dio_)) mark_bad(it.piece);
             return;
         }
         for (uint32_t k = 0; k < it.pieces; ++k) {  // the run failed: piece by piece, as the walk reads
@@ -476,7 +430,7 @@ class Readers {
             if (jobs_[j].next < jobs_[j].items->size()) return (long)j;
         return -1;
     }
-    void loop(bool helper = false) {
+    void loop() {
         std::vector<Seg> segs;
         std::unique_lock<std::mutex> g(mu_);
         for (;;) {
@@ -486,11 +440,9 @@ class Readers {
             Job& j = jobs_[id - base_];
             const ReadItem& it = (*j.items)[j.next++];
             g.unlock();
-            const uint64_t ns = read_item(it, segs, helper);
+            (void)read_item(it, segs);
             g.lock();
             if (--jobs_[id - base_].left == 0) retire();  // the job cannot have retired: left was > 0
-            if (helper && it.len >= (64u << 10) && (double)it.len * 1e9 < kHelperMinRate * (double)ns)
-                return;  // the drive is slower than the page cache could ever be: leave it to the readers
         }
     }
 
@@ -500,8 +452,6 @@ class Readers {
     uint8_t* bad_;
     const uint64_t first_;
     const DirectIo* dio_;
-    cpu_set_t cpus_{};
-    bool pin_ = false;
     std::vector<std::thread> th_;
     std::mutex mu_;
     std::condition_variable cv_, done_cv_;

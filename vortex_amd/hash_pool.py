@@ -33,7 +33,7 @@ from dataclasses import dataclass
 from typing import Any, Optional, Sequence
 
 from . import _lib
-from ._lib import VxError, check, lib, vx_completion, vx_config, vx_stats
+from ._lib import CONFIG_OPTIONS, VxError, check, lib, vx_completion, vx_config, vx_stats
 
 
 @dataclass
@@ -72,10 +72,13 @@ class HashPool:
 
     ``piece_length`` is the torrent's piece_length (the BufferPool buffer
     size, torrent.rs:344).  One HashPool per torrent, used from one thread.
+    ``options`` set the other vx_config fields (include/vx_hash.h, ABI 2):
+    zero_copy, direct_io, batch_chunk, verify_chunk, verify_cold_chunk,
+    verify_ramp; unset ones keep vx_config_default's values.
     """
 
     def __init__(self, piece_length: int, device: int = 0, slots: Optional[int] = None,
-                 batch_pieces: Optional[int] = None, slot_bytes: Optional[int] = None):
+                 batch_pieces: Optional[int] = None, slot_bytes: Optional[int] = None, **options):
         L = lib()
         cfg = vx_config()
         L.vx_config_default(ctypes.byref(cfg), piece_length)
@@ -86,6 +89,10 @@ class HashPool:
             cfg.slot_bytes = slot_bytes
         if batch_pieces is not None:
             cfg.batch_pieces = batch_pieces
+        for name, value in options.items():
+            if name not in CONFIG_OPTIONS:
+                raise TypeError(f"HashPool: unknown option {name!r} (vx_config has {', '.join(CONFIG_OPTIONS)})")
+            setattr(cfg, name, int(value))
         h = ctypes.c_void_p()
         check(L.vx_create(ctypes.byref(cfg), ctypes.byref(h)), "vx_create")
         self._h = h
