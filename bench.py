@@ -22,13 +22,25 @@ Extra fields (DESIGN.md §7 "Measurement"; all but roofline at N=1 only):
                  per-block chain time against its floor.
   e2e            8,192 x 256 KiB host pieces in 8,192 separately registered
                  mmaps (vortex's BufferPool layout) via vx_verify_batch.
-  e2e_async      the same pieces through vx_submit/vx_flush/vx_poll.
+  e2e_async      the same pieces through vx_submit/vx_flush/vx_poll; `paced`:
+                 the download loop at 1/4/16/40 GB/s arrivals (loop-thread
+                 time in the engine, submit stall, submit-to-poll latency).
   e2e_contiguous the same pieces in one registered mmap (best-case layout).
   reverify       config 5: linux-mint-geometry re-verify from an fsync'd,
                  page-cache-warm file via vx_verify_files, with the CPU pool
                  on the same file, and each call's read / copy budget.
   reverify_cold  the same with the file's pages evicted before every call
                  (fsync + POSIX_FADV_DONTNEED): reads from the disk.
+At N > 1 (every rank takes part):
+  ranks          every rank's step / kernel / verdict-gather time, shader
+                 clock, and identity (device index, PCI bus id, UUID, the
+                 world size RCCL reported); distinct_devices must hold unless
+                 --same-device (a rehearsal).
+  reverify_multi config 5 split over the N GPUs by piece index, warm and cold,
+                 the slowest rank's time, beside the CPU pool on every node CPU.
+roofline.valu.clock_run: the shader clock of each XCC over the timed steps
+(s_memtime / s_memrealtime stamps, vortex_amd/csrc/vx_clock.hip) and the
+kernel's issue fraction at that clock.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 N > 1: either launched by the driver as
@@ -240,7 +252,7 @@ def e2e_batch(plen: int, n: int = 8192):
                       f"vx_verify_batch (gather kernel + hash + D2H), median of 3 calls, {el * 1e3:.1f} ms"}
 
 
-def e2e_async(plen: int, n: int = 8192):
+def e2e_async(plen: int, n: int = 8192, cpu_thread_GiBps: float | None = None):
     """The download path end to end: tools/native/async_probe (C++, built by
     build()) submits n pieces from n separately registered mmaps in shuffled
     order with vx_submit, flushes every 64 submits and polls like the event
@@ -266,8 +278,45 @@ def e2e_async(plen: int, n: int = 8192):
             "engine": d.get("engine"),
             "stream_4x": {"GiBps": d4.get("GiBps"), "GiB": round(4 * total_gib, 3), "mismatched": d4.get("mismatched"),
                           "polled": d4.get("polled"), "error": d4.get("error")},
+            "paced": paced_leg(plen, cpu_thread_GiBps=cpu_thread_GiBps),
             "sample": f"{d['pieces']} x {plen // 1024} KiB from {n} separately registered mmaps, shuffled, "
                       f"vx_submit + vx_flush every 64 + vx_poll (tools/native/async_probe)"}
+
+
+def paced_leg(plen: int, rates=(1, 4, 16, 40), seconds: float = 1.0, cpu_thread_GiBps: float | None = None):
+    """The download path at network-realistic arrival rates
+    (tools/native/paced_probe): pieces arrive at R GB/s into a pool of 8,192
+    registered buffers; every 1 ms loop turn submits what arrived, flushes
+    once and polls (peer_connection.rs:1145-1158, event_loop.rs:554-557).
+    Per rate: the loop thread's time inside the engine per second of wall
+    time, vx_stats' submit stall per second, and submit-to-poll latency
+    percentiles; every verdict checked.  vortex's loop waits at most 150 ms
+    per turn (event_loop.rs:438-439).  Beside it, one pool thread's time for
+    one piece (rayon runs a piece per task): plen / the per-thread rate of
+    the CPU baseline measured in this run (or 2.2e9 B/s, SHA-NI, if absent)."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "tools", "native", "paced_probe")
+    if not os.path.exists(exe):
+        return {"error": "tools/native/paced_probe not built"}
+    out = {}
+    for r in rates:
+        p = subprocess.run([exe, str(plen), str(r), str(seconds), "1000", "8192"], capture_output=True, text=True,
+                           timeout=120)
+        if p.returncode != 0:
+            out[f"{r}GBps"] = {"error": f"paced_probe rc={p.returncode}: {p.stderr[-300:]}"}
+            continue
+        d = json.loads(p.stdout.strip().splitlines()[-1])
+        out[f"{r}GBps"] = {k: d[k] for k in ("achieved_GBps", "pieces", "loop_ms_per_s", "submit_ms_per_s",
+                                              "flush_ms_per_s", "poll_ms_per_s", "max_call_ms",
+                                              "submit_stall_ms_per_s", "batches", "latency_ms", "pool_waits",
+                                              "mismatched_verdicts")}
+    rate = cpu_thread_GiBps * GiB if cpu_thread_GiBps else 2.2e9
+    out["cpu_pool_piece_ms"] = {"value": round(plen / rate * 1e3, 4),
+                                "source": "cpu_baseline per-thread rate" if cpu_thread_GiBps else "2.2e9 B/s (SHA-NI)"}
+    out["note"] = ("1 ms loop turns, one vx_flush per turn, 8,192 registered 256 KiB buffers; loop_ms_per_s is the "
+                   "event-loop thread's time inside vx_submit/vx_flush/vx_poll per second")
+    return out
 
 
 def ragged_leg(dev, stream, steps: int = 5):
@@ -555,17 +604,31 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
     node_cpus = len(os.sched_getaffinity(0))
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     io_threads = max(2, min(16, node_cpus // max(1, local_world)))
+
+    # Every step that can fail on one rank only is caught there and agreed on
+    # by all ranks before the next collective, so the ranks fail together and
+    # none waits in a collective the others never reach.
+    def agree(ok: bool) -> bool:
+        flags = [None] * world
+        dist.all_gather_object(flags, bool(ok))
+        return all(flags)
+
     obj = [None]
     if rank == 0:
-        d = reverify_dir()
-        path = os.path.join(d, f"vx_bench_multi_linuxmint_{os.getpid()}.iso")
-        t0 = time.perf_counter()
-        total, n, last = write_linuxmint_file(path, scale)
-        exp = oracle.pool_digest_synth(0x5EED0005, 0, n, 2097152, last_index=n - 1, last_len=last,
-                                       threads=min(node_cpus, 64))
-        obj = [{"path": path, "dir": d, "total": total, "n": n, "exp": exp, "write_s": time.perf_counter() - t0}]
+        try:
+            d = reverify_dir()
+            path = os.path.join(d, f"vx_bench_multi_linuxmint_{os.getpid()}.iso")
+            t0 = time.perf_counter()
+            total, n, last = write_linuxmint_file(path, scale)
+            exp = oracle.pool_digest_synth(0x5EED0005, 0, n, 2097152, last_index=n - 1, last_len=last,
+                                           threads=min(node_cpus, 64))
+            obj = [{"path": path, "dir": d, "total": total, "n": n, "exp": exp, "write_s": time.perf_counter() - t0}]
+        except Exception as e:  # noqa: BLE001  (reported to every rank)
+            obj = [{"error": f"rank 0 could not write the torrent file: {type(e).__name__}: {e}"}]
     dist.broadcast_object_list(obj, src=0)
     spec = obj[0]
+    if "error" in spec:
+        raise RuntimeError(spec["error"])
     path, total, n, exp = spec["path"], spec["total"], spec["n"], spec["exp"]
     pl = 2097152
     first, count = shard.shard_range(n, world, rank)
@@ -573,48 +636,65 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
     legs = {"warm": [], "cold": []}
     traces = {"warm": [], "cold": []}
     cpu = {"warm": [], "cold": []}
-    def agree(flag: bool) -> bool:  # every rank takes the same branch, so no rank waits alone
-        flags = [None] * world
-        dist.all_gather_object(flags, bool(flag))
-        return all(flags)
-
     cpu_ok = True
+    pool = None
     try:
-        with HashPool(pl, device=local, slots=4, slot_bytes=512 << 20, batch_pieces=4096) as pool:
+        try:
+            pool = HashPool(pl, device=local, slots=4, slot_bytes=512 << 20, batch_pieces=4096)
             got, bad = pool.verify_files([path], [total], pl, exp, io_threads=io_threads, first=first, count=count)
-            if not agree(all(got) and bad == 0):
-                raise RuntimeError("multi-GPU re-verify: a rank's warm-up verdicts differ from the expected table")
-            for leg, k in (("warm", reps), ("cold", cold_reps)):
-                for _ in range(k):
-                    if leg == "cold" and rank == 0:
+            ok = all(got) and bad == 0
+        except Exception as e:  # noqa: BLE001
+            log(f"rank {rank}: re-verify setup failed: {type(e).__name__}: {e}")
+            ok = False
+        if not agree(ok):
+            raise RuntimeError("multi-GPU re-verify: a rank failed to open its context or its warm-up verdicts "
+                               "differ from the expected table")
+        for leg, k in (("warm", reps), ("cold", cold_reps)):
+            for _ in range(k):
+                if leg == "cold" and rank == 0:
+                    try:
                         drop_cache(path)
-                    dist.barrier()
+                    except OSError:
+                        pass
+                dist.barrier()
+                try:
                     t0 = time.perf_counter()
                     got, bad = pool.verify_files([path], [total], pl, exp, io_threads=io_threads, first=first,
                                                  count=count)
                     el = time.perf_counter() - t0
                     tr = pool.last_verify()
-                    verdicts = shard.gather_verdicts(torch.tensor(got, dtype=torch.uint8, device=vdev), n)
-                    times = [None] * world
-                    dist.all_gather_object(times, {"s": el, "bad": bad, "read_GiBps": tr["read_GiBps"],
-                                                   "copy_busy_frac": tr["copy_busy_frac"],
-                                                   "direct_bytes": tr["direct_bytes"]})
-                    if int(verdicts.sum()) != n or any(t["bad"] for t in times):  # the same on every rank
-                        raise RuntimeError("multi-GPU re-verify: verdicts differ from the expected table")
-                    if rank == 0:
-                        legs[leg].append(max(t["s"] for t in times))
-                        traces[leg].append([{k2: (round(v, 3) if isinstance(v, float) else v) for k2, v in t.items()}
-                                            for t in times])
-                    # the CPU pool on the whole node, GPU ranks idle at the barrier
-                    if rank == 0:
+                    ok = True
+                except Exception as e:  # noqa: BLE001
+                    log(f"rank {rank}: re-verify call failed: {type(e).__name__}: {e}")
+                    ok = False
+                if not agree(ok):
+                    raise RuntimeError("multi-GPU re-verify: a rank's vx_verify_files_range call failed")
+                verdicts = shard.gather_verdicts(torch.tensor(got, dtype=torch.uint8, device=vdev), n)
+                times = [None] * world
+                dist.all_gather_object(times, {"s": el, "bad": bad, "read_GiBps": tr["read_GiBps"],
+                                               "copy_busy_frac": tr["copy_busy_frac"],
+                                               "direct_bytes": tr["direct_bytes"]})
+                if int(verdicts.sum()) != n or any(t["bad"] for t in times):  # the same on every rank
+                    raise RuntimeError("multi-GPU re-verify: verdicts differ from the expected table")
+                if rank == 0:
+                    legs[leg].append(max(t["s"] for t in times))
+                    traces[leg].append([{k2: (round(v, 3) if isinstance(v, float) else v) for k2, v in t.items()}
+                                        for t in times])
+                    # the CPU pool on the whole node, the GPU ranks idle at the barrier below
+                    try:
                         if leg == "cold":
                             drop_cache(path)
                         t0 = time.perf_counter()
-                        ok = oracle.pool_verify_files([path], [total], pl, exp, threads=node_cpus)
+                        okc = oracle.pool_verify_files([path], [total], pl, exp, threads=node_cpus)
                         cpu[leg].append(time.perf_counter() - t0)
-                        cpu_ok = cpu_ok and all(ok)
-                    dist.barrier()
+                        cpu_ok = cpu_ok and all(okc)
+                    except Exception as e:  # noqa: BLE001  (recorded; the GPU figures stand)
+                        log(f"CPU pool re-verify failed: {type(e).__name__}: {e}")
+                        cpu_ok = False
+                dist.barrier()
     finally:
+        if pool is not None:
+            pool.close()
         dist.barrier()
         if rank == 0 and os.path.exists(path):
             os.unlink(path)
@@ -626,11 +706,13 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
 
     out = {}
     for leg in ("warm", "cold"):
-        g, c = med(legs[leg]), med(cpu[leg])
+        g = med(legs[leg])
+        c = med(cpu[leg]) if cpu[leg] else None
         out[leg] = {"value": round(total / g / GiB, 2), "unit": "GiB/s", "s_runs": [round(t, 4) for t in legs[leg]],
-                    "cpu_pool": {"value": round(total / c / GiB, 2), "unit": "GiB/s", "cores": node_cpus,
-                                 "kind": "port", "s_runs": [round(t, 4) for t in cpu[leg]]},
-                    "gpu_over_cpu": round(c / g, 3), "rank_traces": traces[leg]}
+                    "cpu_pool": None if c is None else {
+                        "value": round(total / c / GiB, 2), "unit": "GiB/s", "cores": node_cpus, "kind": "port",
+                        "s_runs": [round(t, 4) for t in cpu[leg]]},
+                    "gpu_over_cpu": None if c is None else round(c / g, 3), "rank_traces": traces[leg]}
     out.update({"ranks": world, "same_device": same_device, "io_threads_per_rank": io_threads,
                 "pieces": n, "bytes": total, "write_s": round(spec["write_s"], 2), "cpu_pool_verdicts_ok": cpu_ok,
                 "file": {"dir": spec["dir"], "fs": fs_type(spec["dir"])},
@@ -1100,7 +1182,9 @@ def main() -> int:
             leg(("ragged",), ragged_leg, dev, stream)
         if not args.no_e2e:
             leg(("e2e",), e2e_batch, plen)
-            leg(("e2e_async",), e2e_async, plen)
+            cb = res.get("cpu_baseline") or {}
+            per_thread = cb["value"] / cb["cores"] if cb.get("value") and cb.get("cores") else None
+            leg(("e2e_async",), e2e_async, plen, 8192, per_thread)
             leg(("e2e_contiguous",), e2e_contiguous, plen)
         if not args.no_reverify:
             leg(("reverify", "reverify_cold"), reverify_leg)

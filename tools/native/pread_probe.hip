@@ -1,10 +1,14 @@
 // pread_probe.hip — host-side ceiling of the bulk re-verify reader: T threads
-// pread 256 KiB chunks of a (page-cache warm) file into a hipHostMalloc'd
-// stage, as vx_files::Readers does, with no GPU work.  Prints one JSON line.
-// usage: pread_probe <file> [threads...]
-// VX_DMA=1: one more thread streams 512 MiB H2D copies out of a second pinned
-// buffer the whole time (the re-verify's DMA competing for host memory);
-// the DMA rate over the read window is reported beside the read rate.
+// pread chunks of a (page-cache warm) file into a hipHostMalloc'd stage, as
+// vx_files::Readers does, with no GPU work.  Prints one JSON line.
+// usage: pread_probe <file> [threads...] [c=<chunk bytes>...] [p=<piece bytes>] [dma]
+//   c=   read sizes to try (default 262144)
+//   p=   chunk-major order inside pieces of this size, as the re-verify's
+//        resumable rounds read (chunk k of every piece, then chunk k+1; 0 =
+//        the file in order, default)
+//   dma  one more thread streams 512 MiB H2D copies out of a second pinned
+//        buffer the whole time (the re-verify's DMA competing for host
+//        memory); the DMA rate over the read window is reported beside.
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <sys/stat.h>
@@ -24,22 +28,30 @@ int main(int argc, char** argv) {
     if (fd < 0) return 3;
     struct stat st;
     fstat(fd, &st);
-    const size_t bytes = st.st_size, chunk = 256 * 1024;
+    const size_t bytes = st.st_size, chunk = 256 * 1024;  // default read size
     const size_t stage = 512ull << 20;  // one slot's stage, reused round-robin
     uint8_t* buf = nullptr;
     if (hipHostMalloc(&buf, stage, hipHostMallocDefault) != hipSuccess) return 4;
     std::vector<int> ts;
-    for (int i = 2; i < argc; ++i) ts.push_back(std::atoi(argv[i]));
+    std::vector<size_t> chunks;
+    size_t piece = 0;
+    bool dma = false;
+    for (int i = 2; i < argc; ++i) {
+        if (argv[i][0] == 'c' && argv[i][1] == '=') chunks.push_back(std::strtoull(argv[i] + 2, nullptr, 0));
+        else if (argv[i][0] == 'p' && argv[i][1] == '=') piece = std::strtoull(argv[i] + 2, nullptr, 0);
+        else if (std::strcmp(argv[i], "dma") == 0) dma = true;
+        else ts.push_back(std::atoi(argv[i]));
+    }
     if (ts.empty()) ts = {1, 4, 8, 16};
-    const char* de = std::getenv("VX_DMA");
-    const bool dma = de && de[0] == '1';
+    if (chunks.empty()) chunks = {chunk};
     uint8_t *src = nullptr, *dev = nullptr;
     hipStream_t ds = nullptr;
     if (dma && (hipHostMalloc(&src, stage, hipHostMallocDefault) != hipSuccess ||
                 hipMalloc(&dev, stage) != hipSuccess || hipStreamCreate(&ds) != hipSuccess))
         return 5;
     if (dma) std::memset(src, 1, stage);
-    std::printf("{\"file_bytes\": %zu, \"dma\": %d", bytes, (int)dma);
+    std::printf("{\"file_bytes\": %zu, \"dma\": %d, \"piece\": %zu", bytes, (int)dma, piece);
+    for (const size_t C : chunks)
     for (int T : ts) {
         double best = 0, best_dma = 0;
         for (int rep = 0; rep < 3; ++rep) {
@@ -61,12 +73,22 @@ int main(int argc, char** argv) {
             std::vector<std::thread> th;
             for (int t = 0; t < T; ++t)
                 th.emplace_back([&] {
+                    // chunk-major inside pieces: item k is chunk k / npieces of piece k % npieces
+                    const size_t per = piece && piece > C ? piece / C : 1, npieces = piece ? (bytes + piece - 1) / piece : 0;
                     for (;;) {
                         const size_t k = next.fetch_add(1);
-                        const size_t off = k * chunk;
-                        if (off >= bytes) return;
-                        const size_t len = std::min(chunk, bytes - off);
-                        if (pread(fd, buf + (off % stage), len, (off_t)off) != (ssize_t)len) std::abort();
+                        size_t off = k * C;
+                        if (per > 1) {
+                            const size_t r = k / npieces, pc = k % npieces;
+                            if (r >= per) return;
+                            off = pc * piece + r * C;
+                        }
+                        if (off >= bytes) {
+                            if (per > 1) continue;
+                            return;
+                        }
+                        const size_t len = std::min(C, bytes - off);
+                        if (pread(fd, buf + (k * C % stage), len, (off_t)off) != (ssize_t)len) std::abort();
                     }
                 });
             const size_t m0 = moved.load();
@@ -80,8 +102,8 @@ int main(int argc, char** argv) {
                 best_dma = (m1 - m0) / s / (1 << 30);
             }
         }
-        std::printf(", \"pread_GiBps_t%d\": %.2f", T, best);
-        if (dma) std::printf(", \"dma_GiBps_t%d\": %.2f", T, best_dma);
+        std::printf(", \"pread_GiBps_c%zu_t%d\": %.2f", C, T, best);
+        if (dma) std::printf(", \"dma_GiBps_c%zu_t%d\": %.2f", C, T, best_dma);
     }
     std::printf("}\n");
     (void)hipHostFree(buf);
