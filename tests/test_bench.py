@@ -212,3 +212,33 @@ def test_reverify_multi_leg_rehearsal(built, gpu):
     for leg in ("warm", "cold"):
         assert rm[leg]["value"] > 0 and rm[leg]["cpu_pool"]["value"] > 0
         assert all(len(t) == 2 for t in rm[leg]["rank_traces"])
+
+
+@pytest.mark.parametrize("mode", ["ok", "fail"])
+def test_reverify_multi_leg_collective_logic_cpu(tmp_path, mode):
+    """bench.reverify_multi_leg at world size 2 on gloo, no GPU: the engine is
+    replaced by a CPU stand-in that verifies each rank's piece range with the
+    oracle (tests/_multi_leg_rank.py).  "ok": rank 0 reports warm and cold
+    rates from the slowest rank, every verdict gathered.  "fail": rank 1's
+    second timed call raises; both ranks must raise together (no rank left
+    waiting in a collective) and the file must be gone."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = tmp_path / "out.json"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", TMPDIR=str(tmp_path))
+    env.pop("WORLD_SIZE", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "tests", "_multi_leg_rank.py"),
+           str(out), mode]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(out.read_text())
+    if mode == "ok":
+        rm = d["result"]
+        assert rm["ranks"] == 2 and rm["pieces"] == 28 and rm["cpu_pool_verdicts_ok"] is True
+        for leg in ("warm", "cold"):
+            assert rm[leg]["value"] > 0 and all(len(t) == 2 for t in rm[leg]["rank_traces"])
+    else:
+        assert "vx_verify_files_range call failed" in d["error"]
+    assert not [p for p in os.listdir(tmp_path) if p.startswith("vx_bench_multi_linuxmint")]

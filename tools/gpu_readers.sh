@@ -18,7 +18,7 @@ for args in "16 262144 2 4 1 0" "16 262144 2 4 0 0" "16 262144 2 4 1 1" "12 2621
 done
 rm -f $F
 timeout -k 10 400 python -u tools/reverify_ab.py --reps 4 --cold-reps 1 \
-  --configs "t16=;t12=IO_THREADS=12;t8=IO_THREADS=8;t24=IO_THREADS=24" > $OUT/ab.jsonl 2> $OUT/ab.err || { echo AB_FAIL; tail -5 $OUT/ab.err; exit 1; }
+  --configs "t16=;t12=IO_THREADS=12;t8=IO_THREADS=8;t24=IO_THREADS=24;s6=SLOTS=6;s3=SLOTS=3" > $OUT/ab.jsonl 2> $OUT/ab.err || { echo AB_FAIL; tail -5 $OUT/ab.err; exit 1; }
 python3 -c "
 import json
 for l in open('$OUT/ab.jsonl'):

@@ -11,8 +11,8 @@ vx_tuning_last_verify budget, and the CPU pool on the same file.
 
 usage: python tools/reverify_ab.py [--reps 3] [--cold-reps 2] [--configs name=K=V,K=V;...]
 e.g. --configs "default=;cold1m=verify_cold_chunk=1048576;buffered=direct_io=0".
-A configuration's IO_THREADS=N (not a vx_config field) sets its io_threads
-(default: the process's CPU share).
+A configuration's IO_THREADS=N sets its io_threads (default: the process's CPU
+share), SLOTS=N / SLOT_MIB=M its slot count and size (default 4 x 512 MiB).
 """
 import argparse
 import json
@@ -59,7 +59,8 @@ def main():
     path = os.path.join(d, f"vx_ab_linuxmint_{os.getpid()}.iso")
     buf = ctypes.create_string_buffer(pl)
     configs = parse(a.configs)
-    io = {name: int(env.pop("IO_THREADS", 0)) or threads for name, env in configs}
+    io = {name: int(opts.pop("IO_THREADS", 0)) or threads for name, opts in configs}
+    geom = {name: (int(opts.pop("SLOTS", 4)), int(opts.pop("SLOT_MIB", 512))) for name, opts in configs}
     res = {name: {"warm": [], "cold": [], "warm_tr": [], "cold_tr": [], "options": opts, "io_threads": io[name]}
            for name, opts in configs}
     cpu = {"warm": [], "cold": []}
@@ -75,7 +76,7 @@ def main():
         cache_nodes = page_cache_nodes(path)
         pools = {}
         for name, opts in configs:
-            pools[name] = HashPool(pl, slots=4, slot_bytes=512 << 20, batch_pieces=4096,
+            pools[name] = HashPool(pl, slots=geom[name][0], slot_bytes=geom[name][1] << 20, batch_pieces=4096,
                                    **{k: int(v, 0) for k, v in opts.items()})
             got, bad = pools[name].verify_files([path], [total], pl, exp, io_threads=io[name])  # warm-up
             assert all(got) and bad == 0
