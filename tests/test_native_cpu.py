@@ -115,9 +115,11 @@ def test_direct_reads_of_uncached_ranges(tmp_path):
     """vx_files::DirectIo (the re-verify's O_DIRECT path, DESIGN.md §6.1):
     every read returns the file's bytes whatever the alignment; with it
     enabled (vx_config.direct_io = 1) ranges not in the page cache go O_DIRECT
-    (mincore probe) and cached ones do not; disabled, nothing does.
-    resident_fraction (which picks the re-verify's cold chunk) is ~0 on the
-    evicted file, 1 on the cached one, and 1 when nothing is mapped.  A file
+    (mincore probe) and cached ones do not; a file sampled as (nearly) all
+    cached is read buffered with no per-read probe; disabled, nothing goes
+    direct.  resident_fraction (sampled once per call; it picks the re-verify's
+    cold chunk) is ~0 on the evicted file, ~0.5 half cached, 1 on the cached
+    one, and 1 when nothing is mapped.  A file
     renamed over the path after it was opened does not leak into the reads:
     the direct descriptor reopens the open file."""
     d = _disk_dir(tmp_path)
@@ -138,7 +140,10 @@ def test_direct_reads_of_uncached_ranges(tmp_path):
             fd = os.open(path, os.O_RDONLY)
             if evict:
                 os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
-            else:
+            if evict == "half":  # only the first half cached: the file is probed per read
+                os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_RANDOM)  # no readahead past the half
+                os.pread(fd, (8 << 20) // 2, 0)
+            elif not evict:
                 while os.read(fd, 1 << 20):  # fault every page in
                     pass
             os.close(fd)
@@ -159,6 +164,10 @@ def test_direct_reads_of_uncached_ranges(tmp_path):
         assert warm == 0  # cached: buffered
         # evicted pages read direct (the kernel may keep a few pages; most ranges go direct)
         assert cold > 0
+        # half cached: below the warm threshold, so each read is probed; the cached half stays buffered
+        half = run(1, evict="half")
+        assert 0.3 < resident[-1] < 0.9, resident
+        assert 0 < half < cold
         # another file renamed over the path after the open: reads still match the opened file
         other = path + ".new"
         with open(other, "wb") as f:

@@ -122,11 +122,15 @@ struct ReadItem {
 // page cache; at startup the torrent's data is usually not cached, and on the
 // MI355X box a buffered cold pread ran 5-12 GiB/s where O_DIRECT of the same
 // file ran ~20 GiB/s (16 threads, tools/disk_probe.sh, profiles/r03/disk/).
-// Per read: if the first page of the range is not resident (mincore on a
-// PROT_READ mapping of the file, which faults nothing in) and destination,
-// offset and length are 4 KiB aligned, the range goes through an O_DIRECT
-// descriptor; an unaligned tail, a cached range, or a direct read that fails
-// goes through the normal one.  Bytes are the file's either way: the O_DIRECT
+// Once per call, each file's residency is sampled (mincore on a PROT_READ
+// mapping of the file, which faults nothing in).  A file the page cache holds
+// (nearly) whole is read buffered throughout, with no per-read probe: on the
+// MI355X box 16 readers probing every 256 KiB read ran the warm linux-mint
+// file at 43 GiB/s against 81 with plain preads (tools/native/readers_probe,
+// profiles/r04/readers).  Otherwise, per read: if the first page of the range
+// is not resident and destination, offset and length are 4 KiB aligned, the
+// range goes through an O_DIRECT descriptor; an unaligned tail, a cached
+// range, or a direct read that fails goes through the normal one.  Bytes are the file's either way: the O_DIRECT
 // descriptor is a reopen of the caller's own descriptor (/proc/self/fd/N),
 // checked to be the same inode, so a path renamed or replaced after the
 // buffered open can never mix two files' bytes in one piece.
@@ -141,6 +145,8 @@ class DirectIo {
     // descriptors or mappings (vm.max_map_count) in the middle of a call.
     static constexpr uint64_t kMinFile = 1ull << 20;
     static constexpr size_t kMaxFiles = 4096;
+    static constexpr uint64_t kSamples = 256;  // residency samples per call
+    static constexpr double kWarm = 0.9;       // a file this cached is read buffered throughout
     // enabled = false: every read is buffered (vx_config.direct_io = 0).
     DirectIo(const std::vector<int>& fds, bool enabled)
         : dfd_(fds.size(), -1), map_(fds.size(), nullptr), size_(fds.size(), 0) {
@@ -167,6 +173,29 @@ class DirectIo {
             size_[f] = (uint64_t)st.st_size;
             ++used;
         }
+        // Residency, sampled once: about kSamples pages spread over the mapped
+        // files by size (mid-points of equal parts, at least 16 per file).
+        uint64_t total = 0;
+        for (size_t f = 0; f < map_.size(); ++f)
+            if (map_[f]) total += size_[f];
+        uint64_t hit_all = 0, seen_all = 0;
+        for (size_t f = 0; f < map_.size() && total; ++f) {
+            if (!map_[f]) continue;
+            const uint64_t pages = (size_[f] + kBlock - 1) / kBlock;
+            const uint64_t k = std::min<uint64_t>(pages, std::max<uint64_t>(16, kSamples * size_[f] / total));
+            uint64_t hit = 0;
+            for (uint64_t i = 0; i < k; ++i)
+                hit += resident((uint32_t)f, (int64_t)(((2 * i + 1) * pages / (2 * k)) * kBlock)) ? 1 : 0;
+            hit_all += hit;
+            seen_all += k;
+            if ((double)hit >= kWarm * (double)k) {  // cached: buffered reads, no probe, no second descriptor
+                close(dfd_[f]);
+                munmap(map_[f], (size_t)size_[f]);
+                dfd_[f] = -1;
+                map_[f] = nullptr;
+            }
+        }
+        resident_ = seen_all ? (double)hit_all / (double)seen_all : 1.0;
     }
     ~DirectIo() {
         for (size_t f = 0; f < dfd_.size(); ++f) {
@@ -193,27 +222,10 @@ class DirectIo {
     }
     uint64_t direct_bytes() const { return direct_bytes_.load(std::memory_order_relaxed); }
 
-    // Fraction of about `samples` pages, spread over the mapped files by size
-    // (mid-points of equal parts, at least one per file), that the page cache
-    // holds: mincore, no faults.  1 when nothing is mapped (O_DIRECT off, or
-    // no file it applies to), so the caller's warm choice stands.
-    double resident_fraction(uint64_t samples = 256) const {
-        uint64_t total = 0;
-        for (size_t f = 0; f < map_.size(); ++f)
-            if (map_[f]) total += size_[f];
-        if (total == 0 || samples == 0) return 1.0;
-        uint64_t hit = 0, seen = 0;
-        for (size_t f = 0; f < map_.size(); ++f) {
-            if (!map_[f]) continue;
-            const uint64_t pages = (size_[f] + kBlock - 1) / kBlock;
-            const uint64_t k = std::min<uint64_t>(pages, std::max<uint64_t>(1, samples * size_[f] / total));
-            for (uint64_t i = 0; i < k; ++i) {
-                hit += resident((uint32_t)f, (int64_t)(((2 * i + 1) * pages / (2 * k)) * kBlock)) ? 1 : 0;
-                ++seen;
-            }
-        }
-        return seen ? (double)hit / (double)seen : 1.0;
-    }
+    // The sampled fraction of the eligible files' pages the page cache held
+    // when this call began.  1 when no file is eligible (O_DIRECT off, or no
+    // file it applies to), so the caller's warm choice stands.
+    double resident_fraction() const { return resident_; }
 
   private:
     bool resident(uint32_t f, int64_t off) const {
@@ -223,6 +235,7 @@ class DirectIo {
     std::vector<int> dfd_;
     std::vector<void*> map_;
     std::vector<uint64_t> size_;
+    double resident_ = 1.0;
     mutable std::atomic<uint64_t> direct_bytes_{0};
 };
 
