@@ -74,6 +74,22 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def node_cpus() -> int:
+    """CPUs this process may really use on the node: its affinity set, capped by
+    a cgroup v2 CPU quota (cpu.max "quota period") when one is set.  Unlike
+    cpu_share() it ignores OMP_NUM_THREADS, which torch.distributed.run sets
+    to 1 for every rank of a multi-rank launch."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max" and int(period) > 0:
+            n = min(n, max(1, int(quota) // int(period)))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def cpu_share() -> int:
     n = len(os.sched_getaffinity(0))
     env = os.environ.get("OMP_NUM_THREADS")
@@ -601,9 +617,9 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
     from vortex_amd import shard
     from vortex_amd.hash_pool import HashPool
 
-    node_cpus = len(os.sched_getaffinity(0))
+    ncpu = node_cpus()
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    io_threads = max(2, min(16, node_cpus // max(1, local_world)))
+    io_threads = max(2, min(16, ncpu // max(1, local_world)))
 
     # Every step that can fail on one rank only is caught there and agreed on
     # by all ranks before the next collective, so the ranks fail together and
@@ -621,7 +637,7 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
             t0 = time.perf_counter()
             total, n, last = write_linuxmint_file(path, scale)
             exp = oracle.pool_digest_synth(0x5EED0005, 0, n, 2097152, last_index=n - 1, last_len=last,
-                                           threads=min(node_cpus, 64))
+                                           threads=min(ncpu, 64))
             obj = [{"path": path, "dir": d, "total": total, "n": n, "exp": exp, "write_s": time.perf_counter() - t0}]
         except Exception as e:  # noqa: BLE001  (reported to every rank)
             obj = [{"error": f"rank 0 could not write the torrent file: {type(e).__name__}: {e}"}]
@@ -685,7 +701,7 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
                         if leg == "cold":
                             drop_cache(path)
                         t0 = time.perf_counter()
-                        okc = oracle.pool_verify_files([path], [total], pl, exp, threads=node_cpus)
+                        okc = oracle.pool_verify_files([path], [total], pl, exp, threads=ncpu)
                         cpu[leg].append(time.perf_counter() - t0)
                         cpu_ok = cpu_ok and all(okc)
                     except Exception as e:  # noqa: BLE001  (recorded; the GPU figures stand)
@@ -710,7 +726,7 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
         c = med(cpu[leg]) if cpu[leg] else None
         out[leg] = {"value": round(total / g / GiB, 2), "unit": "GiB/s", "s_runs": [round(t, 4) for t in legs[leg]],
                     "cpu_pool": None if c is None else {
-                        "value": round(total / c / GiB, 2), "unit": "GiB/s", "cores": node_cpus, "kind": "port",
+                        "value": round(total / c / GiB, 2), "unit": "GiB/s", "cores": ncpu, "kind": "port",
                         "s_runs": [round(t, 4) for t in cpu[leg]]},
                     "gpu_over_cpu": None if c is None else round(c / g, 3), "rank_traces": traces[leg]}
     out.update({"ranks": world, "same_device": same_device, "io_threads_per_rank": io_threads,
@@ -719,7 +735,7 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
                 "sample": f"config 5 split over {world} ranks by piece index (vx_verify_files_range per rank, own "
                           f"GPU and PCIe link): {n} x 2 MiB pieces ({total} B, linux-mint geometry, synthetic), "
                           f"warm median of {reps}, cold (evicted) median of {cold_reps}; the slowest rank's time; "
-                          f"CPU pool restatement with all {node_cpus} node CPUs beside it"})
+                          f"CPU pool restatement with all {ncpu} node CPUs beside it"})
     return out
 
 
