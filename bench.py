@@ -1056,15 +1056,15 @@ def main() -> int:
         vdev.sha1_uniform(data, n, plen, stride=stride, expected=expected, matched=matched, want_digests=False,
                           stream=stream)
 
+    # everything the timed region needs is set up before the warm-up, so the
+    # warm-up runs right up to the first timed step and the clock it raised holds
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    clk = ClockStamps(dev, stream)
+    ident = device_identity(local)
     for _ in range(args.warmup):
         step()
         if distributed:
             gather_verdicts(matched, n_total)
-    torch.cuda.synchronize()
-
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    clk = ClockStamps(dev, stream)
-    ident = device_identity(local)
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()

@@ -7,7 +7,8 @@
 // the pipeline's copy chain does).  Tells whether the readers bind by
 // themselves or only inside the full pipeline.
 //
-// usage: readers_probe <file> <piece_len> [threads=16] [chunk=262144] [ahead=2] [stages=4] [dio=1] [dma=0] [reps=3]
+// usage: readers_probe <file> <piece_len> [threads=16] [chunk=262144] [ahead=2] [stages=4] [dio=1] [dma=0] [reps=3] [evict=0]
+//   evict=1: drop the file's pages (fsync + POSIX_FADV_DONTNEED) before every rep (a cold re-verify)
 // Prints one JSON line: best GiB/s over reps, the readers' own rate (bytes /
 // summed pread time) and, with dma, the copy rate.
 #include <fcntl.h>
@@ -35,6 +36,7 @@ int main(int argc, char** argv) {
     const bool use_dio = argc > 7 ? std::atoi(argv[7]) != 0 : true;
     const bool dma = argc > 8 ? std::atoi(argv[8]) != 0 : false;
     const int reps = argc > 9 ? std::atoi(argv[9]) : 3;
+    const bool evict = argc > 10 ? std::atoi(argv[10]) != 0 : false;
     const int fd = open(path, O_RDONLY | O_CLOEXEC);
     struct stat st;
     if (fd < 0 || fstat(fd, &st) != 0) return 3;
@@ -54,6 +56,10 @@ int main(int argc, char** argv) {
     const auto fs = vx_files::layout(lens, 1, pl);
     double best = 0, best_own = 0, best_copy = 0;
     for (int rep = 0; rep < reps; ++rep) {
+        if (evict) {
+            (void)fsync(fd);
+            (void)posix_fadvise(fd, 0, 0, POSIX_FADV_DONTNEED);
+        }
         std::vector<uint8_t> bad(n, 0);
         const vx_files::DirectIo dio(fds, use_dio);
         vx_files::Readers rd(threads, fs, fds, pl, bad.data(), 0, use_dio ? &dio : nullptr);
@@ -108,8 +114,9 @@ int main(int argc, char** argv) {
         }
     }
     std::printf("{\"threads\": %d, \"chunk\": %llu, \"ahead\": %zu, \"stages\": %d, \"dio\": %d, \"dma\": %d, "
-                "\"GiBps\": %.2f, \"reader_own_GiBps_per_thread\": %.2f, \"copy_GiBps\": %.2f}\n",
-                threads, (unsigned long long)C, ahead, nst, (int)use_dio, (int)dma, best, best_own, best_copy);
+                "\"evict\": %d, \"GiBps\": %.2f, \"reader_own_GiBps_per_thread\": %.2f, \"copy_GiBps\": %.2f}\n",
+                threads, (unsigned long long)C, ahead, nst, (int)use_dio, (int)dma, (int)evict, best, best_own,
+                best_copy);
     for (auto s : stage) (void)hipHostFree(s);
     if (dev) (void)hipFree(dev);
     close(fd);

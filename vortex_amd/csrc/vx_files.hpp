@@ -124,13 +124,15 @@ struct ReadItem {
 // file ran ~20 GiB/s (16 threads, tools/disk_probe.sh, profiles/r03/disk/).
 // Once per call, each file's residency is sampled (mincore on a PROT_READ
 // mapping of the file, which faults nothing in).  A file the page cache holds
-// (nearly) whole is read buffered throughout, with no per-read probe: on the
-// MI355X box 16 readers probing every 256 KiB read ran the warm linux-mint
-// file at 43 GiB/s against 81 with plain preads (tools/native/readers_probe,
-// profiles/r04/readers).  Otherwise, per read: if the first page of the range
-// is not resident and destination, offset and length are 4 KiB aligned, the
-// range goes through an O_DIRECT descriptor; an unaligned tail, a cached
-// range, or a direct read that fails goes through the normal one.  Bytes are the file's either way: the O_DIRECT
+// (nearly) whole is read buffered throughout, and one it (nearly) lacks goes
+// O_DIRECT for every aligned range, both with no per-read probe: inside the
+// engine a mincore per 256 KiB read cost the warm linux-mint re-verify 13 % at
+// the median (profiles/r04/readers).  Only a partly cached file is probed per
+// read: if the first page of the range is not resident and destination,
+// offset and length are 4 KiB aligned, the range goes through the O_DIRECT
+// descriptor.  An unaligned tail, a cached range, or a direct read that fails
+// goes through the normal descriptor.  (O_DIRECT reads stay coherent with the
+// page cache: the kernel writes back dirty pages of the range first.)  Bytes are the file's either way: the O_DIRECT
 // descriptor is a reopen of the caller's own descriptor (/proc/self/fd/N),
 // checked to be the same inode, so a path renamed or replaced after the
 // buffered open can never mix two files' bytes in one piece.
@@ -147,9 +149,10 @@ class DirectIo {
     static constexpr size_t kMaxFiles = 4096;
     static constexpr uint64_t kSamples = 256;  // residency samples per call
     static constexpr double kWarm = 0.9;       // a file this cached is read buffered throughout
+    static constexpr double kCold = 0.1;       // one this uncached goes O_DIRECT where aligned, unprobed
     // enabled = false: every read is buffered (vx_config.direct_io = 0).
     DirectIo(const std::vector<int>& fds, bool enabled)
-        : dfd_(fds.size(), -1), map_(fds.size(), nullptr), size_(fds.size(), 0) {
+        : dfd_(fds.size(), -1), map_(fds.size(), nullptr), size_(fds.size(), 0), cold_(fds.size(), 0) {
         if (!enabled) return;
         size_t used = 0;
         for (size_t f = 0; f < fds.size() && used < kMaxFiles; ++f) {
@@ -193,6 +196,10 @@ class DirectIo {
                 munmap(map_[f], (size_t)size_[f]);
                 dfd_[f] = -1;
                 map_[f] = nullptr;
+            } else if ((double)hit <= kCold * (double)k) {  // not cached: aligned reads go direct, no probe
+                munmap(map_[f], (size_t)size_[f]);
+                map_[f] = nullptr;
+                cold_[f] = 1;
             }
         }
         resident_ = seen_all ? (double)hit_all / (double)seen_all : 1.0;
@@ -211,7 +218,7 @@ class DirectIo {
         const bool aligned = f < dfd_.size() && dfd_[f] >= 0 && len >= (int64_t)kBlock && off >= 0 &&
                              ((reinterpret_cast<uintptr_t>(dst) | (uint64_t)off) & (kBlock - 1)) == 0 &&
                              (uint64_t)(off + len) <= size_[f];
-        if (aligned && !resident(f, off)) {
+        if (aligned && (cold_[f] || !resident(f, off))) {
             const int64_t head = len & ~(int64_t)(kBlock - 1);
             if (read_full(dfd_[f], dst, off, head)) {
                 direct_bytes_.fetch_add((uint64_t)head, std::memory_order_relaxed);
@@ -235,6 +242,7 @@ class DirectIo {
     std::vector<int> dfd_;
     std::vector<void*> map_;
     std::vector<uint64_t> size_;
+    std::vector<uint8_t> cold_;  // sampled as (nearly) uncached: no per-read probe
     double resident_ = 1.0;
     mutable std::atomic<uint64_t> direct_bytes_{0};
 };
