@@ -1051,20 +1051,44 @@ def main() -> int:
     vdev.synth_fill(data, n, plen, stride=stride, first=first, seed=seed, corrupt_every=corrupt_every)
     matched = torch.empty(n, dtype=torch.uint8, device=dev)
     n_total = n * world
+    # On RCCL each step's verdict all-gather runs on the collective stream while
+    # the next step hashes: verdicts alternate between two buffers, and a step
+    # waits (on the device) only for the gather that read its buffer two steps
+    # before.  Every step is still hashed, verified and gathered.  (gloo gathers
+    # host copies synchronously: shard.gather_verdicts.)
+    overlap = distributed and backend == "nccl"
+    mbuf = [matched, torch.empty_like(matched)]
+    gathered = [torch.empty(n_total, dtype=torch.uint8, device=dev) for _ in range(2)] if overlap else None
+    works = [None, None]
 
-    def step():
-        vdev.sha1_uniform(data, n, plen, stride=stride, expected=expected, matched=matched, want_digests=False,
-                          stream=stream)
+    def step(buf=None):
+        vdev.sha1_uniform(data, n, plen, stride=stride, expected=expected,
+                          matched=matched if buf is None else buf, want_digests=False, stream=stream)
+
+    def before_step(k):
+        if overlap and works[k % 2] is not None:
+            works[k % 2].wait()  # device-side: the gather of step k-2 has read mbuf[k % 2]
+
+    def after_step(k):
+        """Start (RCCL) or do (gloo) step k's verdict gather; the gathered table, or None."""
+        if overlap:
+            works[k % 2] = dist.all_gather_into_tensor(gathered[k % 2], mbuf[k % 2], async_op=True)
+            return None
+        return gather_verdicts(matched, n_total) if distributed else None
 
     # everything the timed region needs is set up before the warm-up, so the
     # warm-up runs right up to the first timed step and the clock it raised holds
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     clk = ClockStamps(dev, stream)
     ident = device_identity(local)
-    for _ in range(args.warmup):
-        step()
-        if distributed:
-            gather_verdicts(matched, n_total)
+    for k in range(args.warmup):
+        before_step(k)
+        step(mbuf[k % 2] if overlap else None)
+        after_step(k)
+    for w in works:
+        if w is not None:
+            w.wait()
+    works[:] = [None, None]
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
@@ -1072,11 +1096,17 @@ def main() -> int:
     verdicts = None
     clk.stamp(0)  # two 256-workgroup stamp launches bracket the steps (~10 us each)
     for k in range(args.steps):
+        before_step(k)
         evs[k][0].record(stream)
-        step()
+        step(mbuf[k % 2] if overlap else None)
         evs[k][1].record(stream)
-        if distributed:
-            verdicts = gather_verdicts(matched, n_total)
+        g = after_step(k)
+        verdicts = g if g is not None else verdicts
+    for w in works:  # the last gathers are part of the timed work
+        if w is not None:
+            w.wait()
+    if overlap:
+        verdicts = gathered[(args.steps - 1) % 2]
     clk.stamp(1)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
