@@ -234,6 +234,20 @@ def _cold_direct_reads(tmp_path, pl, cold_chunk, direct_ok, direct_io):
             elif direct_ok:
                 assert tr["direct_bytes"] > 0
                 assert tr["chunk_bytes"] == ((cold_chunk or 256 * 1024) if chunked else 0), tr
+        # half cached: each file's first half in the page cache, the second not -> the
+        # file is probed per read; the uncached aligned ranges go direct, verdicts unchanged
+        evict()
+        for p in paths:
+            fd = os.open(p, os.O_RDONLY)
+            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_RANDOM)  # no readahead past the half
+            size = os.fstat(fd).st_size
+            os.pread(fd, size // 2, 0)
+            os.close(fd)
+        got, bad = pool.verify_files(paths, sizes, pl, exp, io_threads=4)
+        tr = pool.last_verify()
+        assert got == want and bad == 0
+        if direct_io and direct_ok:
+            assert 0 < tr["direct_bytes"] < sum(sizes), tr
         # cached now (the buffered reads above filled part of it; read the rest): no direct reads
         for p in paths:
             with open(p, "rb") as f:

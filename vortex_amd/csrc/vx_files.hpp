@@ -177,7 +177,8 @@ class DirectIo {
             ++used;
         }
         // Residency, sampled once: about kSamples pages spread over the mapped
-        // files by size (mid-points of equal parts, at least 16 per file).
+        // files by size (mid-points of equal parts, at least 2 per file, so a
+        // torrent of kMaxFiles files costs ~8,000 mincore calls, not 65,000).
         uint64_t total = 0;
         for (size_t f = 0; f < map_.size(); ++f)
             if (map_[f]) total += size_[f];
@@ -185,7 +186,7 @@ class DirectIo {
         for (size_t f = 0; f < map_.size() && total; ++f) {
             if (!map_[f]) continue;
             const uint64_t pages = (size_[f] + kBlock - 1) / kBlock;
-            const uint64_t k = std::min<uint64_t>(pages, std::max<uint64_t>(16, kSamples * size_[f] / total));
+            const uint64_t k = std::min<uint64_t>(pages, std::max<uint64_t>(2, kSamples * size_[f] / total));
             uint64_t hit = 0;
             for (uint64_t i = 0; i < k; ++i)
                 hit += resident((uint32_t)f, (int64_t)(((2 * i + 1) * pages / (2 * k)) * kBlock)) ? 1 : 0;
