@@ -74,14 +74,14 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def node_cpus() -> int:
+def node_cpus(cpu_max: str = "/sys/fs/cgroup/cpu.max") -> int:
     """CPUs this process may really use on the node: its affinity set, capped by
     a cgroup v2 CPU quota (cpu.max "quota period") when one is set.  Unlike
     cpu_share() it ignores OMP_NUM_THREADS, which torch.distributed.run sets
     to 1 for every rank of a multi-rank launch."""
     n = len(os.sched_getaffinity(0))
     try:
-        with open("/sys/fs/cgroup/cpu.max") as f:
+        with open(cpu_max) as f:
             quota, period = f.read().split()[:2]
         if quota != "max" and int(period) > 0:
             n = min(n, max(1, int(quota) // int(period)))

@@ -242,3 +242,21 @@ def test_reverify_multi_leg_collective_logic_cpu(tmp_path, mode):
     else:
         assert "vx_verify_files_range call failed" in d["error"]
     assert not [p for p in os.listdir(tmp_path) if p.startswith("vx_bench_multi_linuxmint")]
+
+
+def test_node_cpus_honours_cgroup_quota(tmp_path):
+    """The multi-GPU leg sizes its readers and CPU pool from the affinity set
+    capped by a cgroup v2 quota, not from OMP_NUM_THREADS (torchrun sets it
+    to 1 per rank)."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    aff = len(os.sched_getaffinity(0))
+    q = tmp_path / "cpu.max"
+    q.write_text("max 100000\n")
+    assert bench.node_cpus(str(q)) == aff
+    q.write_text("200000 100000\n")
+    assert bench.node_cpus(str(q)) == min(aff, 2)
+    q.write_text("50000 100000\n")
+    assert bench.node_cpus(str(q)) == 1
+    assert bench.node_cpus(str(tmp_path / "absent")) == aff
