@@ -615,7 +615,7 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
 
     import oracle
     from vortex_amd import shard
-    from vortex_amd.hash_pool import HashPool
+    from vortex_amd.hash_pool import HashPool, plan_verify
 
     ncpu = node_cpus()
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
@@ -729,6 +729,16 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
                         "value": round(total / c / GiB, 2), "unit": "GiB/s", "cores": ncpu, "kind": "port",
                         "s_runs": [round(t, 4) for t in cpu[leg]]},
                     "gpu_over_cpu": None if c is None else round(c / g, 3), "rank_traces": traces[leg]}
+    # What vx_plan_verify_gpus predicts for this split, with the pool's measured
+    # per-thread rate: each rank's pieces are one lane each, so a 2 MiB piece's
+    # chain (~25 ms) floors a call however many GPUs share the file.
+    cw = med(cpu["warm"]) if cpu["warm"] else None
+    p = plan_verify(n, pl, total, cpu_threads=ncpu, cpu_thread_rate=total / cw / ncpu if cw else 0.0, n_gpus=world)
+    out["plan"] = {"gpu_s": round(p["gpu_s"], 5), "gpu_chain_s": round(p["gpu_chain_s"], 5),
+                   "gpu_transfer_s": round(p["gpu_transfer_s"], 5), "cpu_s": round(p["cpu_s"], 5),
+                   "use_gpu": p["use_gpu"], "predicted_GiBps": round(total / p["gpu_s"] / GiB, 2),
+                   "model": "vx_plan_verify_gpus (DESIGN.md §6.6), n_gpus = ranks, the CPU pool's measured warm "
+                            "rate per thread"}
     out.update({"ranks": world, "same_device": same_device, "io_threads_per_rank": io_threads,
                 "pieces": n, "bytes": total, "write_s": round(spec["write_s"], 2), "cpu_pool_verdicts_ok": cpu_ok,
                 "file": {"dir": spec["dir"], "fs": fs_type(spec["dir"])},

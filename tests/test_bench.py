@@ -212,6 +212,14 @@ def test_reverify_multi_leg_rehearsal(built, gpu):
     for leg in ("warm", "cold"):
         assert rm[leg]["value"] > 0 and rm[leg]["cpu_pool"]["value"] > 0
         assert all(len(t) == 2 for t in rm[leg]["rank_traces"])
+    _check_plan(rm)
+
+
+def _check_plan(rm):
+    """The record's model prediction: one 2 MiB piece's chain floors the call."""
+    p = rm["plan"]
+    assert 0.02 < p["gpu_chain_s"] < 0.03 and p["gpu_s"] >= p["gpu_chain_s"]
+    assert p["cpu_s"] > 0 and isinstance(p["use_gpu"], bool) and p["predicted_GiBps"] > 0
 
 
 @pytest.mark.parametrize("mode", ["ok", "fail"])
@@ -239,6 +247,7 @@ def test_reverify_multi_leg_collective_logic_cpu(tmp_path, mode):
         assert rm["ranks"] == 2 and rm["pieces"] == 28 and rm["cpu_pool_verdicts_ok"] is True
         for leg in ("warm", "cold"):
             assert rm[leg]["value"] > 0 and all(len(t) == 2 for t in rm[leg]["rank_traces"])
+        _check_plan(rm)
     else:
         assert "vx_verify_files_range call failed" in d["error"]
     assert not [p for p in os.listdir(tmp_path) if p.startswith("vx_bench_multi_linuxmint")]
