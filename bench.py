@@ -999,6 +999,8 @@ def main() -> int:
     ap.add_argument("--no-reverify", action="store_true", help="skip the config-5 legs (N=1 and N>1)")
     ap.add_argument("--reverify-multi-scale", type=float, default=1.0,
                     help="N>1 re-verify leg: fraction of linux-mint's pieces (rehearsals)")
+    ap.add_argument("--reverify-multi", action="store_true",
+                    help="run the N>1 re-verify leg even at world size 1, in place of the N=1 one (tests)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL on ROCm, the real path) or gloo (single-GPU multi-rank rehearsal)")
     ap.add_argument("--same-device", action="store_true",
@@ -1194,11 +1196,13 @@ def main() -> int:
     }
     if ranks is not None:
         res["ranks"] = ranks
-    if distributed and world > 1 and not args.no_reverify:
-        # config 5 across the node's GPUs: the one configuration where
-        # several PCIe links can beat the node's own CPU pool; every rank takes part
+    multi = distributed and (world > 1 or args.reverify_multi) and not args.no_reverify
+    extra = rank == 0 and world == 1
+    if multi or extra:
         del data, matched, expected
         torch.cuda.empty_cache()
+    if multi:
+        # config 5 split over the node's GPUs; every rank takes part
         try:
             rm = reverify_multi_leg(rank, world, local, dev, backend, args.same_device, args.reverify_multi_scale)
         except Exception as e:  # noqa: BLE001  (recorded in the line; the checks raise on every rank alike)
@@ -1209,13 +1213,11 @@ def main() -> int:
         if rank == 0:
             res["reverify_multi"] = rm
             log("reverify_multi:", {k: rm[k].get("value") for k in ("warm", "cold")} if "warm" in rm else rm)
-    if rank == 0 and world == 1:
+    if extra:
         # Extra legs (N=1 only): the other BASELINE configs and
         # the host-resident path, each with its own correctness check.  A leg
         # that fails (its check, or the host: disk space, pinning limits) is
         # recorded as {"error": ...} in its key; the metric line still prints.
-        del data, matched, expected
-        torch.cuda.empty_cache()
         log(f"config 2: {value:.1f} GiB/s, kernel {kern_ms:.3f} ms")
 
         def leg(keys, fn, *a):
@@ -1242,7 +1244,7 @@ def main() -> int:
             per_thread = cb["value"] / cb["cores"] if cb.get("value") and cb.get("cores") else None
             leg(("e2e_async",), e2e_async, plen, 8192, per_thread)
             leg(("e2e_contiguous",), e2e_contiguous, plen)
-        if not args.no_reverify:
+        if not args.no_reverify and not multi:
             leg(("reverify", "reverify_cold"), reverify_leg)
     if rank == 0:
         print(json.dumps(res), flush=True)

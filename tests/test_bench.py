@@ -174,6 +174,32 @@ def test_bench_rccl_world_size_1(built, gpu):
     assert 1.0 < clk["GHz_mean"] < 3.0 and clk["one_wave_issue_at_run_clock"]["frac"] > 0
 
 
+@pytest.mark.gpu
+def test_reverify_multi_leg_rccl_world_size_1(built, gpu):
+    """The N>1 config-5 leg on RCCL (verdicts gathered on the device, identity
+    and times through nccl's all_gather_object), at the one world size the box
+    allows for RCCL: what the driver's 8-GPU run takes, minus the other ranks."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    args = ["--pieces", "1024", "--steps", "2", "--warmup", "1", "--no-e2e", "--no-ragged", "--no-cpu-baseline",
+            "--reverify-multi", "--reverify-multi-scale", "0.05"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr=127.0.0.1", f"--master-port={port}", BENCH, "--gpus", "1"] + args
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    (res,) = _lines(r.stdout)
+    assert res["backend"] == "nccl" and "reverify" not in res
+    rm = res["reverify_multi"]
+    assert "error" not in rm, rm
+    assert rm["ranks"] == 1 and rm["same_device"] is False and rm["cpu_pool_verdicts_ok"] is True
+    assert rm["pieces"] == 70
+    for leg in ("warm", "cold"):
+        assert rm[leg]["value"] > 0 and all(len(t) == 1 for t in rm[leg]["rank_traces"])
+    _check_plan(rm)
+
+
 def test_clock_from_stamps():
     """Per-XCC clock = shader cycles / real-time ticks x the tick rate, each XCC
     against its own counters (their offsets differ)."""
