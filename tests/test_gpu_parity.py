@@ -502,7 +502,8 @@ def test_verify_files_chunked(built, gpu, tmp_path, pl, slot_mib, batch):
                                            (131072, 0, (1 << 20) + 3072), (4096, 1, 300000),
                                            (0, 1, 300000), (0, 1, 2 << 20), (0, 1, 262144),
                                            (65536, 3, (1 << 20) + 3072), (65536, 2, (1 << 20) + 3072),
-                                           (0, 0, 2 << 20), (8192, 5, 300000)])
+                                           (0, 0, 2 << 20), (8192, 5, 300000),
+                                           (131072, 1, 262144), (65536, 2, 131072), (1 << 20, 1, 2 << 20)])
 def test_verify_files_chunk_schedule(built, gpu, tmp_path, chunk, ramp, pl):
     """Re-verify round schedules: other chunk sizes
     (vx_config.verify_chunk; 0 = the per-call policy, verify_chunk_for), and

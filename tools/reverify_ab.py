@@ -80,7 +80,7 @@ def main():
                                    **{k: int(v, 0) for k, v in opts.items()})
             got, bad = pools[name].verify_files([path], [total], pl, exp, io_threads=io[name])  # warm-up
             assert all(got) and bad == 0
-        for leg, reps in (("warm", a.reps), ("cold", a.cold_reps)):
+        for leg, reps in (("warm", 0 if a.cold_only else a.reps), ("cold", a.cold_reps)):
             for _ in range(reps):
                 for name, _env in configs:
                     if leg == "cold":

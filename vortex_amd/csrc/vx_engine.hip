@@ -1306,7 +1306,7 @@ std::vector<std::pair<uint64_t, uint64_t>> chunk_schedule(uint64_t L, uint64_t C
     const uint64_t q = C >> (d + 1);
     uint64_t a = 0;
     if (L == 0) r.push_back({0, 0});
-    const bool ramp = d > 0 && q >= 64 && L > 2 * C;
+    const bool ramp = d > 0 && q >= 64 && L >= 2 * C;  // head (ends at C) and tail (from >= C) never overlap
     if (ramp && head) {
         r.push_back({a, q});
         a += q;
