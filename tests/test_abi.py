@@ -218,7 +218,10 @@ def test_chunk_schedule_known(built):
     got = _schedule(2048 * KiB, 256 * KiB, 1, 1)
     assert [l // KiB for _, l in got] == [64, 64, 128] + [256] * 6 + [128, 64, 64]
     assert _schedule(2048 * KiB, 256 * KiB, 0, 0) == [(k * 256 * KiB, 256 * KiB) for k in range(8)]
-    assert _schedule(256 * KiB, 128 * KiB, 1, 1) == [(0, 128 * KiB), (128 * KiB, 128 * KiB)]  # L = 2C: no ramp
+    # L = 2C: head and tail ramps meet at C (round 4; before, such pieces ended on a whole-C chain)
+    assert [l // KiB for _, l in _schedule(256 * KiB, 128 * KiB, 1, 1)] == [32, 32, 64, 64, 32, 32]
+    # below 2C the two ramps would overlap: plain chunks
+    assert _schedule(252 * KiB, 128 * KiB, 1, 1) == [(0, 128 * KiB), (128 * KiB, 124 * KiB)]
     assert _schedule(0, 256 * KiB, 1, 1) == [(0, 0)]  # an empty piece still gets its one padding round
 
 
