@@ -600,6 +600,58 @@ def test_random_mix_all_paths(built, gpu, seed):
         assert [raw[20 * i:20 * i + 20] for i in range(len(lens))] == want
 
 
+@pytest.mark.parametrize("pl", [16 << 20, 32 << 20])
+def test_long_pieces_all_paths(built, gpu, tmp_path, pl):
+    """Piece lengths at BitTorrent's large end (16 and 32 MiB; vortex takes the
+    piece length from the torrent as it is, piece_selector.rs:63-69): host
+    batches (plain bytes, and a registered mmap), async spawn / try_recv, and
+    the file re-verify over two files split mid-piece, with a short last piece
+    and one mismatch, against hashlib and the oracle's re-verify."""
+    import mmap
+
+    from vortex_amd.hash_pool import HashPool
+
+    lens = [pl] * 4 + [pl // 3 + 17]
+    bodies = [oracle.gen_piece(31, i, L) for i, L in enumerate(lens)]
+    want = [hashlib.sha1(b).digest() for b in bodies]
+    exp = list(want)
+    exp[2] = bytes(20)
+    verdicts = [e == w for e, w in zip(exp, want)]
+    offs, o = [], 0
+    for L in lens:
+        offs.append(o)
+        o += (L + 4095) // 4096 * 4096
+    mm = mmap.mmap(-1, o)
+    for off, b in zip(offs, bodies):
+        mm[off:off + len(b)] = b
+    data = b"".join(bodies)
+    cut = pl + 12345  # the second piece straddles the two files
+    paths = [str(tmp_path / "a.bin"), str(tmp_path / "b.bin")]
+    for p, part in zip(paths, (data[:cut], data[cut:])):
+        with open(p, "wb") as f:
+            f.write(part)
+    sizes = [cut, len(data) - cut]
+    with HashPool(pl, slots=3, batch_pieces=8, slot_bytes=2 * pl) as pool:
+        assert pool.sha1_batch(bodies) == want
+        pool.register_buffer(mm)
+        views = [memoryview(mm)[off:off + L] for off, L in zip(offs, lens)]
+        matched, dig = pool.verify_batch(views, exp)
+        assert list(dig) == want and list(matched) == verdicts
+        for i, v in enumerate(views):
+            pool.spawn(i, 7, v, lens[i], exp[i])
+        pool.flush()
+        pool.drain()
+        got = {r.index: r for r in pool.try_iter()}
+        assert sorted(got) == list(range(len(lens)))
+        for i, r in got.items():
+            assert r.digest == want[i] and r.hash_matched == verdicts[i] and r.conn_id == 7
+        del views
+        pool.unregister_buffer(mm)
+        files, bad = pool.verify_files(paths, sizes, pl, b"".join(exp), io_threads=4)
+        assert list(files) == verdicts and bad == 0
+    assert oracle.pool_verify_files(paths, sizes, pl, b"".join(exp), threads=4) == verdicts
+
+
 def test_two_contexts_two_threads(built, gpu):
     """Several torrents at once: one context each (different piece lengths),
     driven from two threads concurrently, async spawns and sync batches mixed.
