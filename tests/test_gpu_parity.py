@@ -652,6 +652,55 @@ def test_long_pieces_all_paths(built, gpu, tmp_path, pl):
     assert oracle.pool_verify_files(paths, sizes, pl, b"".join(exp), threads=4) == verdicts
 
 
+def test_zero_piece_calls(built, gpu, tmp_path):
+    """Calls with nothing to hash return at once and leave the context usable
+    (a torrent whose files are all empty has no pieces; file_store.rs:108-165):
+    empty host batches; flush / drain / poll with nothing queued; re-verifies
+    of zero pieces (no files, one empty file), an empty range of a real
+    torrent and the multi-context form over zero pieces; device batches of
+    zero pieces.  Then real pieces still verify on the same contexts."""
+    import torch
+
+    from vortex_amd import device as vdev
+    from vortex_amd.hash_pool import HashPool, verify_files_multi
+
+    empty = tmp_path / "empty.bin"
+    empty.write_bytes(b"")
+    one = tmp_path / "one.bin"
+    body = oracle.gen_piece(3, 0, 5000)
+    one.write_bytes(body)
+    d = hashlib.sha1(body).digest()
+    pl = 262144
+    with HashPool(pl, slots=2, batch_pieces=8) as pool, HashPool(pl, slots=2, batch_pieces=8) as pool2:
+        assert pool.sha1_batch([]) == []
+        assert pool.verify_batch([], []) == ([], [])
+        pool.flush()
+        pool.drain()
+        assert pool.try_iter() == [] and pool.try_recv() is None and pool.pending == 0
+        assert pool.verify_files([], [], pl, b"") == ([], 0)
+        assert pool.verify_files([str(empty)], [0], pl, b"") == ([], 0)
+        assert pool.verify_files([str(one)], [5000], pl, d, first=0, count=0) == ([], 0)
+        assert pool.verify_files([str(one)], [5000], pl, d, first=1, count=0) == ([], 0)
+        assert verify_files_multi([pool, pool2], [str(empty)], [0], pl, b"") == ([], 0)
+        assert pool.verify_files([str(empty), str(one)], [0, 5000], pl, d) == ([True], 0)
+        assert verify_files_multi([pool, pool2], [str(one)], [5000], pl, d) == ([True], 0)
+        assert pool.verify_batch([body], [d]) == ([True], [d])
+        pool.spawn(0, 1, bytearray(body), len(body), d)
+        pool.drain()
+        (r,) = pool.try_iter()
+        assert r.hash_matched and r.digest == d
+    data = torch.zeros(64, dtype=torch.uint8, device=gpu)
+    dig, _ = vdev.sha1_uniform(data, 0, 64, stride=64)
+    off = torch.zeros(0, dtype=torch.int64, device=gpu)
+    lens = torch.zeros(0, dtype=torch.int32, device=gpu)
+    rdig, _ = vdev.sha1_ragged(data, off, lens)
+    torch.cuda.synchronize()
+    assert dig.numel() == 0 and rdig.numel() == 0
+    dig, _ = vdev.sha1_uniform(data, 1, 64, stride=64)  # the device path still runs
+    torch.cuda.synchronize()
+    assert bytes(dig.cpu().numpy().tobytes()) == hashlib.sha1(bytes(64)).digest()
+
+
 def test_two_contexts_two_threads(built, gpu):
     """Several torrents at once: one context each (different piece lengths),
     driven from two threads concurrently, async spawns and sync batches mixed.
