@@ -555,7 +555,15 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3):
     def record(leg):
         gpu_t, cpu_t, traces, resident = legs[leg]
         g, c = sorted(gpu_t)[len(gpu_t) // 2], sorted(cpu_t)[len(cpu_t) // 2]
-        return {"value": round(total / g / GiB, 2), "unit": "GiB/s", "gpu_s_runs": [round(t, 4) for t in gpu_t],
+        # what bound this box's calls: the H2D copies busy nearly
+        # all the time = PCIe; copies waiting on the readers = the host's reads
+        cb = sorted(t["copy_busy_frac"] for t in traces if t.get("copy_busy_frac") is not None)
+        cbm = cb[len(cb) // 2] if cb else None
+        bound = None if cbm is None else (
+            "pcie (H2D copies busy >= 0.95 of the call)" if cbm >= 0.95 else
+            f"host reads (H2D copies busy {cbm:.2f}: waiting on {'the disk' if leg == 'cold' else 'page-cache reads'})")
+        return {"value": round(total / g / GiB, 2), "unit": "GiB/s", "bound": bound,
+                "gpu_s_runs": [round(t, 4) for t in gpu_t],
                 "cpu_pool": {"value": round(total / c / GiB, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
                              "s_runs": [round(t, 4) for t in cpu_t]},
                 "gpu_over_cpu": round(c / g, 3),

@@ -9,6 +9,6 @@ python3 -c "
 import json; d=json.loads(open('$OUT/bench.json').read().splitlines()[-1])
 print('value', d['value'], 'clock', d['roofline']['valu']['clock_run'].get('GHz_mean'))
 for k in ('cpu_baseline','ragged','e2e','e2e_async','e2e_contiguous','reverify','reverify_cold'):
-    print(k, d.get(k, {}).get('value', d.get(k)))
+    print(k, d.get(k, {}).get('value', d.get(k)), d.get(k, {}).get('bound', ''))
 print(json.dumps(d['e2e_async'].get('paced'), indent=0)[:3000])
 "
