@@ -153,6 +153,33 @@ def test_plain_bench_launches_its_ranks(built, gpu, n):
     assert all(d["world_size"] == n and d["pci_bus_id"] == rk["devices"][0]["pci_bus_id"] for d in rk["devices"])
     assert rk["distinct_devices"] is False
     assert all(1.0 < g < 3.0 for g in rk["clock_GHz"])
+    # every gathered verdict checked, clean pieces against the CPU pool's digests
+    assert res["parity"]["checked"] == n * 1024 and res["config"]["parity_checked"] == n * 1024
+    corrupt = sum(1 for i in range(n * 1024) if i % 100 == 99)
+    assert res["parity"]["corrupt_mismatched"] == corrupt and res["parity"]["bit_exact"] == n * 1024 - corrupt
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_config4_full_size_8_ranks(built, gpu):
+    """BASELINE config 4 at full size on the box's one GPU: 8 gloo ranks x
+    65,536 x 256 KiB = 524,288 pieces (128 GiB in one GPU's HBM), global piece
+    indices r*65536 + i.  Each rank's expected table is the CPU pool
+    restatement's digests of its clean pieces (oracle/pool_oracle.cpp, the
+    par_iter of torrent.rs:724-740 split by index), so the check on the
+    gathered table — exactly the 1 % corrupted pieces mismatch — proves all
+    519,046 clean digests bit-exact against vortex's pool."""
+    args = ["--gpus", "8", "--same-device", "--dist-backend", "gloo", "--pieces", "65536", "--steps", "2",
+            "--warmup", "1", "--no-e2e", "--no-ragged", "--no-reverify", "--no-cpu-baseline"]
+    r = _run(args, timeout=840)
+    assert r.returncode == 0, r.stderr[-3000:]
+    (res,) = _lines(r.stdout)
+    assert res["n_gpus"] == 8 and res["world_size"] == 8 and res["config"]["pieces_per_gpu"] == 65536
+    assert res["config"]["total_GiB"] == 128.0
+    p = res["parity"]
+    corrupt = sum(1 for i in range(8 * 65536) if i % 100 == 99)
+    assert p["checked"] == 524288 and p["corrupt_mismatched"] == corrupt and p["bit_exact"] == 524288 - corrupt
+    assert res["config"]["parity_checked"] == 524288
 
 
 @pytest.mark.gpu
@@ -171,7 +198,10 @@ def test_bench_rccl_world_size_1(built, gpu):
     assert len(res["ranks"]["verdict_gather_ms"]) == 1 and res["ranks"]["verdict_gather_ms"][0] > 0
     assert res["ranks"]["distinct_devices"] is True and res["ranks"]["devices"][0]["world_size"] == 1
     clk = res["roofline"]["valu"]["clock_run"]
-    assert 1.0 < clk["GHz_mean"] < 3.0 and clk["one_wave_issue_at_run_clock"]["frac"] > 0
+    assert 1.0 < clk["GHz_mean"] < 3.0 and 0 < clk["kernel_busy_frac"] <= 1.0
+    frac = clk["one_wave_issue_at_run_clock"]["frac"]  # null when gathers fill > 0.1 of the stamped span
+    assert (frac is None) == (clk["kernel_busy_frac"] < 0.9) and (frac is None or frac > 0)
+    assert res["roofline"]["clock_GHz_run"] == clk["GHz_mean"]
 
 
 @pytest.mark.gpu
@@ -227,7 +257,8 @@ def test_reverify_multi_leg_rehearsal(built, gpu):
     every verdict is gathered and checked (a wrong one raises on every rank),
     and the CPU pool restatement runs beside it with every host CPU."""
     args = ["--pieces", "1024", "--steps", "2", "--warmup", "1", "--no-e2e", "--no-ragged", "--no-cpu-baseline",
-            "--gpus", "2", "--same-device", "--dist-backend", "gloo", "--reverify-multi-scale", "0.05"]
+            "--gpus", "2", "--same-device", "--dist-backend", "gloo", "--reverify-multi",
+            "--reverify-multi-scale", "0.05"]
     r = _run(args, timeout=400)
     assert r.returncode == 0, r.stderr[-3000:]
     (res,) = _lines(r.stdout)
@@ -295,3 +326,26 @@ def test_node_cpus_honours_cgroup_quota(tmp_path):
     q.write_text("50000 100000\n")
     assert bench.node_cpus(str(q)) == 1
     assert bench.node_cpus(str(tmp_path / "absent")) == aff
+
+
+def test_roofline_scalars_for_the_record():
+    """The driver keeps only the scalar fields of `roofline`: the clock the
+    run held and the kernel's fraction of its binding (VALU-issue) roof must
+    be top-level scalars there, not only inside the nested `valu` dict."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    clock = {"GHz_mean": 2.2, "GHz_min": 2.1, "GHz_max": 2.3, "span_ms": 100.0, "GHz_per_xcc": {}}
+    r = bench.roofline(65536, 262144, 4.9, 65536 * 262144 / 4.9e-3, "w", clock, steps=20)
+    for k in ("bound", "achieved", "peak", "unit", "frac", "kernel_ms", "algorithmic_bytes_per_launch",
+              "clock_GHz_run", "clock_GHz_run_min", "clock_kernel_busy_frac", "valu_Tops",
+              "valu_issue_frac_run_clock", "valu_issue_frac_nominal"):
+        assert isinstance(r[k], (int, float, str)) and not isinstance(r[k], bool), k
+    assert r["clock_GHz_run"] == 2.2 and r["clock_GHz_run_min"] == 2.1
+    assert r["clock_kernel_busy_frac"] == pytest.approx(0.98)
+    ops = 65536 * 4097 * 613.5 / 4.9e-3
+    assert r["valu_issue_frac_run_clock"] == pytest.approx(ops / (1024 * 16 * 2.2e9), abs=1e-4)
+    assert r["valu_issue_frac_nominal"] == pytest.approx(ops / (1024 * 16 * 2.4e9), abs=1e-4)
+    # a span the kernels fill only half of (gathers, N > 1): the mean clock is not theirs
+    r2 = bench.roofline(65536, 262144, 4.9, 1.0, "w", dict(clock, span_ms=196.0), steps=20)
+    assert r2["clock_kernel_busy_frac"] == pytest.approx(0.5) and r2["valu_issue_frac_run_clock"] is None
