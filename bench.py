@@ -171,7 +171,7 @@ def e2e_contiguous(plen: int, n: int = 8192):
     import torch
 
     import oracle
-    from vortex_amd._lib import check, lib
+    from vortex_amd._lib import check
     from vortex_amd.hash_pool import HashPool
 
     buf = mmap.mmap(-1, n * plen)
@@ -185,12 +185,12 @@ def e2e_contiguous(plen: int, n: int = 8192):
     digests = ctypes.create_string_buffer(20 * n)
     with HashPool(plen, slots=4, slot_bytes=256 << 20, batch_pieces=1024) as pool:
         pool.register_buffer(buf)
-        check(lib().vx_verify_batch(pool._h, ptrs, lens, exp, 256, matched, digests), "warm")
+        check(pool.lib.vx_verify_batch(pool._h, ptrs, lens, exp, 256, matched, digests), "warm")
         runs = []
         for _ in range(3):
             ctypes.memset(matched, 0, n)
             t0 = time.perf_counter()
-            check(lib().vx_verify_batch(pool._h, ptrs, lens, exp, n, matched, digests), "vx_verify_batch")
+            check(pool.lib.vx_verify_batch(pool._h, ptrs, lens, exp, n, matched, digests), "vx_verify_batch")
             runs.append(time.perf_counter() - t0)
             assert matched.raw[:n] == b"\x01" * n
         pool.unregister_buffer(buf)
@@ -220,7 +220,7 @@ def e2e_batch(plen: int, n: int = 8192):
     buffer's device mapping, then the hash kernels run; verdicts and digests
     come back (PCIe-inclusive end to end)."""
     import oracle
-    from vortex_amd._lib import check, lib
+    from vortex_amd._lib import check
     from vortex_amd.hash_pool import HashPool
 
     bufs = [mmap.mmap(-1, plen) for _ in range(n)]
@@ -236,13 +236,13 @@ def e2e_batch(plen: int, n: int = 8192):
         t0 = time.perf_counter()
         _register_all(pool, bufs)
         t_reg = time.perf_counter() - t0
-        check(lib().vx_verify_batch(pool._h, ptrs, lens, exp, 256, matched, digests), "warm")
+        check(pool.lib.vx_verify_batch(pool._h, ptrs, lens, exp, 256, matched, digests), "warm")
         pool.reset_stats()
         runs = []
         for _ in range(3):
             ctypes.memset(matched, 0, n)
             t0 = time.perf_counter()
-            check(lib().vx_verify_batch(pool._h, ptrs, lens, exp, n, matched, digests), "vx_verify_batch")
+            check(pool.lib.vx_verify_batch(pool._h, ptrs, lens, exp, n, matched, digests), "vx_verify_batch")
             runs.append(time.perf_counter() - t0)
             assert matched.raw[:n] == b"\x01" * n
         st = pool.stats()
@@ -253,7 +253,7 @@ def e2e_batch(plen: int, n: int = 8192):
         exp4 = ctypes.create_string_buffer(exp.raw * 4, 20 * n4)
         matched4 = ctypes.create_string_buffer(n4)
         t0 = time.perf_counter()
-        check(lib().vx_verify_batch(pool._h, ptrs4, lens4, exp4, n4, matched4, None), "vx_verify_batch x4")
+        check(pool.lib.vx_verify_batch(pool._h, ptrs4, lens4, exp4, n4, matched4, None), "vx_verify_batch x4")
         el4 = time.perf_counter() - t0
         assert matched4.raw[:n4] == b"\x01" * n4
         _unregister_all(pool, bufs)
@@ -348,7 +348,7 @@ def ragged_leg(dev, stream, steps: int = 5):
 
     import oracle
     from vortex_amd import device as vdev
-    from vortex_amd._lib import lib
+    from vortex_amd._lib import tuning
 
     classes = [(16384, 262144), (262144, 16384), (1 << 20, 4096), (4 << 20, 1024)]
     seed_base = 0x5EED0003
@@ -368,7 +368,7 @@ def ragged_leg(dev, stream, steps: int = 5):
     d_len = torch.from_numpy(lens).to(dev)
     order = vdev.length_order(lens).to(dev)
     plan = vdev.ragged_plan(lens)
-    variant = int(lib().vx_tuning_plan_ragged(n, plan[0], plan[1]))
+    variant = int(tuning().vx_tuning_plan_ragged(n, plan[0], plan[1]))
     with torch.cuda.stream(stream):
         dig, _ = vdev.sha1_ragged(data, d_off, d_len, order=order, plan=plan, stream=stream)  # validates the layout
     torch.cuda.synchronize()
@@ -486,7 +486,87 @@ def reverify_dir() -> str:
     return next(d for d in cands if d and os.path.isdir(d) and os.access(d, os.W_OK))
 
 
-def reverify_leg(reps: int = 5, cold_reps: int = 3):
+def copy_gaps(rounds: list, min_ms: float = 0.02) -> dict:
+    """Where the copy engine sat idle inside one re-verify call, from its round
+    timeline (HashPool.last_verify_rounds, vx_last_verify_rounds).  For every
+    gap between round k-1's copy end and round k's copy start: "read" when
+    round k's reads finished after round k-1's copy had ended (the readers
+    were late), "hand-off" when they had finished but round k was enqueued
+    after it (the loop thread was waiting elsewhere: an earlier round's
+    reads, a free slot), else "device" (enqueued in time, started late:
+    stream order).  ramp: round k is a shortened head/tail round."""
+    from vortex_amd._lib import VX_ROUND_HEAD_RAMP, VX_ROUND_TAIL_RAMP
+
+    gaps = []
+    for k in range(1, len(rounds)):
+        a, b = rounds[k - 1], rounds[k]
+        if not a["copy_end_ms"] or not b["copy_start_ms"]:
+            continue
+        g = b["copy_start_ms"] - a["copy_end_ms"]
+        if g <= min_ms:
+            continue
+        cause = "read" if b["read_done_ms"] > a["copy_end_ms"] else (
+            "hand-off" if b["enqueue_ms"] > a["copy_end_ms"] else "device")
+        gaps.append({"round": k, "gap_ms": round(g, 3), "cause": cause,
+                     "ramp": bool(b["flags"] & (VX_ROUND_HEAD_RAMP | VX_ROUND_TAIL_RAMP)),
+                     "read_late_ms": round(b["read_done_ms"] - a["copy_end_ms"], 3),
+                     "enqueue_late_ms": round(b["enqueue_ms"] - a["copy_end_ms"], 3)})
+    by = {}
+    for g in gaps:
+        by[g["cause"]] = round(by.get(g["cause"], 0.0) + g["gap_ms"], 3)
+    first = rounds[0]["copy_start_ms"] if rounds and rounds[0]["copy_start_ms"] else None
+    return {"gap_ms": round(sum(g["gap_ms"] for g in gaps), 3), "by_cause": by,
+            "ramp_gap_ms": round(sum(g["gap_ms"] for g in gaps if g["ramp"]), 3),
+            "worst": sorted(gaps, key=lambda g: -g["gap_ms"])[:3], "rounds": len(rounds),
+            "first_copy_start_ms": None if first is None else round(first, 3)}
+
+
+def split_call(pool, path: str, total: int, n: int, pl: int, exp: bytes, first: int, io_threads: int,
+               cpu_threads: int) -> dict:
+    """One bulk re-verify split between the GPU and vortex's pool, both at
+    once (INTEGRATION.md "Split"): the engine verifies pieces [first, n)
+    with vx_verify_files_range while the CPU restatement of vortex's own
+    re-verify (oracle/pool_oracle.cpp, the par_iter of torrent.rs:724-740;
+    the pool's stand-in, kind "port", as in `cpu_pool`) verifies [0, first)
+    on cpu_threads threads.  ctypes drops the GIL in both calls, so they run
+    concurrently.  Returns wall time, each side's time and verdict check."""
+    import threading
+
+    import oracle
+
+    res, errs = {}, []
+
+    def gpu():
+        try:
+            t0 = time.perf_counter()
+            got, bad = pool.verify_files([path], [total], pl, exp, io_threads=io_threads, first=first,
+                                         count=n - first)
+            res["gpu"] = (all(got) and bad == 0, time.perf_counter() - t0)
+        except Exception as e:  # noqa: BLE001  (raised below, on the calling thread)
+            errs.append(e)
+
+    def cpu():
+        try:
+            t0 = time.perf_counter()
+            ok = oracle.pool_verify_files([path], [total], pl, exp[:20 * first], threads=cpu_threads)
+            res["cpu"] = (all(ok) and len(ok) == first, time.perf_counter() - t0)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = ([threading.Thread(target=gpu)] if first < n else []) + ([threading.Thread(target=cpu)] if first else [])
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    wall = time.perf_counter() - t0
+    if errs:
+        raise errs[0]
+    ok = all(v[0] for v in res.values())
+    return {"s": wall, "gpu_s": res.get("gpu", (True, 0.0))[1], "cpu_s": res.get("cpu", (True, 0.0))[1], "ok": ok}
+
+
+def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 5):
     """BASELINE config 5: full re-verify of a torrent's data from disk with
     the linux-mint geometry (cli/linux-mint.torrent: 2,907,832,320 B, 2 MiB
     pieces, last 1,179,648 B) through vx_verify_files (pread into pinned
@@ -505,7 +585,7 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3):
     Each GPU call's time budget (vx_tuning_last_verify: reader busy time and
     rate, GPU-timed copy busy fraction) goes into the record."""
     import oracle
-    from vortex_amd.hash_pool import HashPool
+    from vortex_amd.hash_pool import HashPool, plan_verify_split
 
     pl = 2097152
     threads = cpu_share()
@@ -518,7 +598,11 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3):
         keep = ("wall_ms", "read_busy_ms", "read_span_ms", "first_read_ms", "copy_busy_ms", "copy_span_ms", "tail_ms",
                 "read_GiBps", "read_GiBps_per_thread", "copy_GiBps", "copy_busy_frac", "rounds", "readers",
                 "direct_bytes", "chunk_bytes")
-        return {k: (round(tr[k], 3) if isinstance(tr[k], float) else tr[k]) for k in keep}
+        out = {k: (round(tr[k], 3) if isinstance(tr[k], float) else tr[k]) for k in keep}
+        rounds = pool.last_verify_rounds()
+        out["copy_gaps"] = copy_gaps(rounds)
+        out["timeline"] = [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()} for r in rounds]
+        return out
 
     try:
         total, n, last = write_linuxmint_file(path)
@@ -549,6 +633,23 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3):
                     assert all(cpu)
                 legs[leg] = (gpu_t, cpu_t, traces, resident)
             st = pool.stats()
+            # the split (vx_plan_verify_split with the pool's per-thread rate just measured), warm
+            for _ in range(2):
+                resident_fraction(path)  # cached again after the cold leg: read it once through
+                oracle.pool_verify_files([path], [total], pl, exp, threads=threads)
+            cw = sorted(legs["warm"][1])[len(legs["warm"][1]) // 2]
+            plan = plan_verify_split(n, pl, total, cpu_threads=threads, cpu_thread_rate=total / cw / threads)
+            split = {"plan": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in plan.items()},
+                     "configs": []}
+            for io_t, cpu_th in ((threads, threads), (max(2, threads // 2), threads)):
+                calls = [split_call(pool, path, total, n, pl, exp, plan["gpu_first"], io_t, cpu_th)
+                         for _ in range(split_reps)]
+                assert all(c["ok"] for c in calls), "split re-verify: a verdict differs from the expected table"
+                med = sorted(calls, key=lambda c: c["s"])[len(calls) // 2]
+                split["configs"].append({"io_threads": io_t, "cpu_threads": cpu_th,
+                                         "value": round(total / med["s"] / GiB, 2),
+                                         "s_runs": [round(c["s"], 4) for c in calls],
+                                         "gpu_s": round(med["gpu_s"], 4), "cpu_s": round(med["cpu_s"], 4)})
     finally:
         if os.path.exists(path):
             os.unlink(path)
@@ -563,7 +664,13 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3):
         bound = None if cbm is None else (
             "pcie (H2D copies busy >= 0.95 of the call)" if cbm >= 0.95 else
             f"host reads (H2D copies busy {cbm:.2f}: waiting on {'the disk' if leg == 'cold' else 'page-cache reads'})")
+        # the median call's copy-engine gaps by cause (its full timeline stays in gpu_traces)
+        med_trace = traces[sorted(range(len(gpu_t)), key=lambda i: gpu_t[i])[len(gpu_t) // 2]]
+        for t in traces:  # one full timeline (the median call's) is enough for the record
+            if t is not med_trace:
+                t.pop("timeline", None)
         return {"value": round(total / g / GiB, 2), "unit": "GiB/s", "bound": bound,
+                "copy_gaps": med_trace.get("copy_gaps"),
                 "gpu_s_runs": [round(t, 4) for t in gpu_t],
                 "cpu_pool": {"value": round(total / c / GiB, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
                              "s_runs": [round(t, 4) for t in cpu_t]},
@@ -572,6 +679,16 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3):
                 "gpu_traces": traces}
 
     warm, cold = record("warm"), record("cold")
+    best = max(split["configs"], key=lambda c: c["value"])
+    split.update({"value": best["value"], "unit": "GiB/s", "gpu_only": warm["value"],
+                  "pool_only": warm["cpu_pool"]["value"],
+                  "beats_both": best["value"] > max(warm["value"], warm["cpu_pool"]["value"]),
+                  "pool_kind": "port",
+                  "sample": f"the warm file split by vx_plan_verify_split: GPU pieces [{split['plan']['gpu_first']}, {n}) "
+                            f"via vx_verify_files_range while the CPU pool restatement (vortex's par_iter stand-in) "
+                            f"verifies [0, {split['plan']['gpu_first']}) at once; median of {split_reps} per "
+                            f"(engine readers, pool threads) config; every verdict checked"})
+    warm["split"] = split
     where = {"dir": d, "fs": fs_type(d)}
     warm.update({"write_s": round(t_write, 2), "file": where,
                  "engine": {k: st[k] for k in ("pieces_completed", "bytes_completed", "batches", "chunk_rounds",
@@ -915,17 +1032,17 @@ class ClockStamps:
     def __init__(self, dev, stream):
         import torch
 
-        from vortex_amd._lib import lib
+        from vortex_amd._lib import tuning
 
         self.stream, self.dev = stream, dev
         self.buf = [torch.zeros(3 * CLOCK_BLOCKS, dtype=torch.int64, device=dev) for _ in range(2)]
-        self.khz = lib().vx_tuning_wall_clock_khz(dev.index or 0)
+        self.khz = tuning().vx_tuning_wall_clock_khz(dev.index or 0)
 
     def stamp(self, k: int) -> None:
-        from vortex_amd._lib import check, lib
+        from vortex_amd._lib import check, tuning
 
-        check(lib().vx_tuning_clock_stamp(self.buf[k].data_ptr(), CLOCK_BLOCKS, self.stream.cuda_stream),
-              "vx_tuning_clock_stamp")
+        check(tuning().vx_tuning_clock_stamp(self.buf[k].data_ptr(), CLOCK_BLOCKS, self.stream.cuda_stream),
+              "vx_tuning_clock_stamp", tuning())
 
     def result(self) -> dict:
         if self.khz <= 0:
@@ -935,11 +1052,11 @@ class ClockStamps:
 
 def device_identity(local: int) -> dict:
     """Which physical GPU this rank hashed on (PCI bus id, UUID)."""
-    from vortex_amd._lib import check, lib
+    from vortex_amd._lib import check, tuning
 
     bus = ctypes.create_string_buffer(64)
     uuid = ctypes.create_string_buffer(16)
-    check(lib().vx_tuning_device_identity(local, bus, 64, uuid), "vx_tuning_device_identity")
+    check(tuning().vx_tuning_device_identity(local, bus, 64, uuid), "vx_tuning_device_identity", tuning())
     return {"device_index": local, "pci_bus_id": bus.value.decode().lower(), "uuid": uuid.raw.hex(),
             "visible_devices": {k: os.environ[k] for k in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES",
                                                           "CUDA_VISIBLE_DEVICES") if k in os.environ}}

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define VX_ABI_VERSION 2
+#define VX_ABI_VERSION 3
 
 /* Error codes (negative errno values). */
 #define VX_OK 0
@@ -79,7 +79,8 @@ typedef struct vx_completion {
 
 /* Everything a caller may choose is here; the engine reads no environment
  * variables.  Start from vx_config_default() and change fields (ABI 2 added
- * the six after slot_bytes; vx_create rejects values outside their ranges). */
+ * the six after slot_bytes; vx_create rejects values outside their ranges,
+ * chunk sizes above 1 GiB included). */
 typedef struct vx_config {
     int32_t device;             /* HIP device ordinal                                   */
     uint32_t max_piece_len;     /* bytes; torrent piece_length (torrent.rs:344 pool size) */
@@ -215,9 +216,60 @@ typedef struct vx_stats {
     uint64_t batch_latency_sum_us; /* first submit of a batch -> its results harvested, summed           */
     uint64_t batch_latency_max_us;
     uint64_t batch_latency_hist[VX_STATS_HIST]; /* batches per [2^k, 2^(k+1)) us; [0] holds < 2 us, the last bucket everything longer */
+    uint64_t zero_copy_slots;     /* (ABI 3) batches hashed straight out of registered host memory (§6.5)  */
+    uint64_t zero_copy_loader_slots; /* (ABI 3) ... of them in the three-wave form (slots of < 128 pieces) */
 } vx_stats;
 int vx_get_stats(const vx_ctx* ctx, vx_stats* out);
 int vx_reset_stats(vx_ctx* ctx);
+
+/* Where the last vx_verify_files / _range call on ctx spent its time: the
+ * startup re-verify's budget an operator sees (reads, PCIe copies, the tail).
+ * Host times are steady-clock; copy times are the GPU's own (events around
+ * each data H2D) and exist only on the resumable chunk path (pieces >= 2
+ * chunks). */
+typedef struct vx_verify_trace {
+    double wall_ms;        /* the whole call                                          */
+    double read_busy_ms;   /* pread time summed over the reader threads               */
+    double read_span_ms;   /* first read started -> last read finished                */
+    double first_read_ms;  /* call start -> first read finished (nothing overlaps it) */
+    double copy_busy_ms;   /* GPU-timed data copies, summed (chunk path)              */
+    double copy_span_ms;   /* first copy start -> last copy end, GPU clock            */
+    double tail_ms;        /* last round enqueued -> verdicts on the host             */
+    uint64_t read_bytes;   /* bytes pread                                             */
+    uint64_t copy_bytes;   /* bytes of the timed copies                               */
+    uint32_t readers;      /* reader threads                                          */
+    uint32_t rounds;       /* timed copies (chunk rounds)                             */
+    uint64_t direct_bytes; /* of read_bytes, read with O_DIRECT (not cached; §6.1)    */
+    uint64_t chunk_bytes;  /* chunk of the resumable rounds (0: whole-piece slots)    */
+} vx_verify_trace;
+int vx_last_verify(const vx_ctx* ctx, vx_verify_trace* out);
+
+/* The same call's round timeline (chunk path; none on the whole-piece path):
+ * one record per round, in enqueue order, every time in ms from the call's
+ * start on the host's steady clock.  GPU times are mapped onto it through an
+ * event recorded on an idle stream at the call's start (error: that event's
+ * dispatch latency, tens of us).  A gap on the copy engine between round k-1's
+ * copy_end_ms and round k's copy_start_ms is the reads' when round k's
+ * read_done_ms came after it, the hand-off's when its enqueue_ms did, and
+ * otherwise the device's (stream dependencies). */
+#define VX_ROUND_NEW_WINDOW 1u /* first round of a window of pieces              */
+#define VX_ROUND_HEAD_RAMP 2u  /* a shortened round of the call's first chunk     */
+#define VX_ROUND_TAIL_RAMP 4u  /* a shortened round of the call's last chunk      */
+typedef struct vx_verify_round {
+    double read_submit_ms; /* its reads queued on the reader pool                 */
+    double read_done_ms;   /* its last read finished                              */
+    double enqueue_ms;     /* its data copy and chunk kernel enqueued              */
+    double copy_start_ms;  /* GPU: its data copy began (0 when not timed)         */
+    double copy_end_ms;    /* GPU: its data copy ended                            */
+    double kernel_end_ms;  /* GPU: its chunk kernel ended                         */
+    uint64_t bytes;        /* bytes copied                                        */
+    uint64_t offset;       /* the chunk's offset inside its pieces                */
+    uint32_t lanes;        /* pieces in the round                                 */
+    uint32_t flags;        /* VX_ROUND_*                                          */
+} vx_verify_round;
+/* Writes up to max records to out (may be NULL with max 0) and returns how
+ * many rounds the call had. */
+int64_t vx_last_verify_rounds(const vx_ctx* ctx, vx_verify_round* out, size_t max);
 
 /* ---- synchronous host batches (bulk re-verify, torrent.rs:724-740) ----- */
 /* digests_out: n*20 bytes.  Pieces are pipelined through the slots, longest
@@ -294,6 +346,19 @@ int vx_plan_verify(uint64_t n_pieces, uint32_t piece_length, uint64_t total_leng
  * n_gpus 0 or 1 gives vx_plan_verify's answer. */
 int vx_plan_verify_gpus(uint64_t n_pieces, uint32_t piece_length, uint64_t total_length, uint32_t cpu_threads,
                         double cpu_thread_rate, uint32_t n_gpus, vx_plan* out);
+/* Split one bulk verify between the GPUs and the caller's own pool, both
+ * running at once (torrent.rs:724-740's par_iter over the pool's range, and
+ * vx_verify_files_range / _multi over the GPUs' range): the GPUs take the
+ * contiguous tail [*gpu_first, n_pieces), *gpu_count pieces, chosen so the
+ * predicted GPU time (the same model, over n_gpus) equals the pool's time on
+ * the rest; the last piece (the short one) goes to whichever side holds the
+ * tail.  *gpu_count is 0 when the pool alone is faster than any split, and
+ * n_pieces when the GPUs alone are.  out (may be NULL) gets the plan of the
+ * split: gpu_s for the GPUs' range, cpu_s for the pool's, use_gpu = 1 when
+ * the split beats both sides alone by the 10 % margin. */
+int vx_plan_verify_split(uint64_t n_pieces, uint32_t piece_length, uint64_t total_length, uint32_t cpu_threads,
+                         double cpu_thread_rate, uint32_t n_gpus, uint64_t* gpu_first, uint64_t* gpu_count,
+                         vx_plan* out);
 
 /* ---- device-resident batches (the hot path; no context needed) --------
  * These entries validate what they can see on the host — NULL pointers, the

@@ -1,13 +1,18 @@
 /*
- * vx_tuning.h — kernel-variant selection for A/B measurement (not part of
- * the drop-in boundary).  vx_sha1_device_uniform() always runs the default
- * (best measured) variant; this entry point lets tools/ and tests pin one.
- *   0 = default, 1 = lane-per-piece (one wave per 64 pieces does loads,
- *   schedule and rounds), 2 = producer/consumer split (a load+schedule wave
- *   feeds a rounds-only wave through an LDS ring), 3 / 4 = split with a 2- / 3-slot
- *   LDS ring (A/B of the ring protocol; 2 uses the default ring), 5 = split
- *   with one pair per CU (ragged only; what the planner picks for batches
- *   bound by their longest chain).
+ * vx_tuning.h — measurement and test entry points, NOT part of the drop-in
+ * boundary.  They are exported only by the test/tuning build
+ * libvortex_amd_tuning.so (the same sources, linked with -DVX_TEST_HOOKS);
+ * the library vortex links, libvortex_amd.so, exports vx_hash.h alone
+ * (tests/test_abi.py checks both export lists with nm -D).  Unstable: these
+ * may change in any release without an ABI version bump.
+ *
+ * Kernel variants (vx_sha1_device_*_variant): 0 = default (what
+ * vx_sha1_device_uniform / _ragged run), 1 = lane-per-piece (one wave per 64
+ * pieces does loads, schedule and rounds), 2 = producer/consumer split (a
+ * load+schedule wave feeds a rounds-only wave through an LDS ring), 3 / 4 =
+ * split with a 2- / 3-slot LDS ring (A/B of the ring protocol; 2 uses the
+ * default ring), 5 = split with one pair per CU (ragged only; what the
+ * planner picks for batches bound by their longest chain).
  */
 #ifndef VX_TUNING_H
 #define VX_TUNING_H
@@ -20,21 +25,7 @@ extern "C" {
 int vx_sha1_device_ragged_variant(const void* d_base, const uint64_t* d_offsets, const uint32_t* d_lens,
                                   const uint32_t* d_order, uint32_t n, void* d_digests, const void* d_expected,
                                   void* d_matched, void* stream, int variant);
-/* Chunk rounds a context has launched on the resumable chunk paths (file
- * re-verify of pieces >= 2 chunks, strided host batches).
- * Tests use it to tell which path a batch took. */
 struct vx_ctx;
-uint64_t vx_tuning_chunk_rounds(const struct vx_ctx* ctx);
-/* 64 KiB tiles the context's gather kernel has pulled from registered host
- * buffers (async / batch slots). */
-uint64_t vx_tuning_gather_tiles(const struct vx_ctx* ctx);
-/* Slots the context hashed with the zero-copy kernel (every piece registered
- * and aligned, read from host memory by the hash kernel itself, no gather;
- * DESIGN.md §6.5). */
-uint64_t vx_tuning_zero_copy_slots(const struct vx_ctx* ctx);
-/* ... of them, the slots hashed in the three-wave form (a loader wave beside
- * the pair; what the policy picks for slots of fewer than 128 pieces). */
-uint64_t vx_tuning_zero_copy_loader_slots(const struct vx_ctx* ctx);
 /* How a context with zero_copy = 1 hashes a slot of n registered, aligned
  * pieces of total_len bytes: 1 the zero-copy pair, 2 the zero-copy kernel
  * with a loader wave (n < 128, a latency-bound batch); 0 (gather + hash) is
@@ -64,27 +55,6 @@ int vx_tuning_plan_ragged(uint32_t n, uint32_t max_len, uint64_t total_len);
  * C/4).  Writes up to max (offset, length) pairs to out
  * (2*max uint64_t) and returns the number of rounds (host-only). */
 size_t vx_tuning_chunk_schedule(uint64_t L, uint64_t C, int head, int tail, uint64_t* out, size_t max);
-
-/* Where the last vx_verify_files / vx_verify_files_range call on ctx spent
- * its time (bench.py records it per timed call).  Host times
- * are steady-clock; copy times are the GPU's own (events around each data
- * H2D) and exist only on the resumable chunk path (pieces >= 2 chunks). */
-typedef struct vx_verify_trace {
-    double wall_ms;        /* the whole call                                          */
-    double read_busy_ms;   /* pread time summed over the reader threads               */
-    double read_span_ms;   /* first read started -> last read finished                */
-    double first_read_ms;  /* call start -> first read finished (nothing overlaps it) */
-    double copy_busy_ms;   /* GPU-timed data copies, summed (chunk path)              */
-    double copy_span_ms;   /* first copy start -> last copy end, GPU clock            */
-    double tail_ms;        /* last round enqueued -> verdicts on the host             */
-    uint64_t read_bytes;   /* bytes pread                                             */
-    uint64_t copy_bytes;   /* bytes of the timed copies                               */
-    uint32_t readers;      /* reader threads                                          */
-    uint32_t rounds;       /* timed copies (chunk rounds)                             */
-    uint64_t direct_bytes; /* of read_bytes, read with O_DIRECT (not cached; §6.1)    */
-    uint64_t chunk_bytes;  /* chunk of the resumable rounds (0: whole-piece slots)    */
-} vx_verify_trace;
-int vx_tuning_last_verify(const struct vx_ctx* ctx, vx_verify_trace* out);
 
 int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
                                    const void* d_expected, void* d_matched, void* stream, int variant);

@@ -10,13 +10,19 @@ import pytest
 from conftest import ROOT
 
 
-def declared_symbols():
+def declared_symbols(headers=("vx_hash.h",)):
     names = set()
-    for h in ("vx_hash.h", "vx_synth.h", "vx_tuning.h"):
+    for h in headers:
         src = open(os.path.join(ROOT, "include", h)).read()
         src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
         names |= set(re.findall(r"\b(vx_[a-z0-9_]+)\s*\(", src))
     return names
+
+
+def dynamic_symbols(path):
+    """Every defined dynamic symbol of a shared library (nm -D)."""
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
 
 
 def test_headers_compile_as_c(tmp_path):
@@ -71,20 +77,46 @@ def test_stats_layout(tmp_path):
                                        vx_stats.batch_latency_hist.offset, VX_STATS_HIST)
 
 
+@pytest.mark.parametrize("struct,fields", [
+    ("vx_verify_trace", None), ("vx_verify_round", None), ("vx_stats", ("zero_copy_slots", "zero_copy_loader_slots")),
+    ("vx_plan", None)])
+def test_observability_layouts(tmp_path, struct, fields):
+    """ABI 3's observability structs as ctypes have the C layout: size and
+    every field's offset (vx_stats: the two fields ABI 3 appended)."""
+    from vortex_amd import _lib
+
+    cls = getattr(_lib, struct)
+    names = list(fields or [n for n, _ in cls._fields_])
+    c = tmp_path / "o.c"
+    body = ", ".join(f"offsetof({struct}, {f})" for f in names)
+    c.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "vx_hash.h"\nint main(void){size_t o[] = {'
+                 + body + '}; printf("%zu", sizeof(' + struct + ')); for (size_t i = 0; i < sizeof(o) / sizeof(o[0]); '
+                 '++i) printf(" %zu", o[i]); printf("\\n"); return 0;}\n')
+    exe = tmp_path / "o"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), str(c), "-o",
+                    str(exe)], check=True)
+    got = list(map(int, subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()))
+    assert got == [ctypes.sizeof(cls)] + [getattr(cls, f).offset for f in names]
+
+
 def test_library_exports_declared_symbols(built):
+    """The release library vortex links exports exactly the functions of
+    vx_hash.h — no test hooks, no kernel-variant pins, no C++ internals (VERDICT
+    r4 #6) — and the tuning build exports vx_hash.h + vx_tuning.h + vx_synth.h."""
     from vortex_amd import _lib
 
     lib = _lib.lib()
     decl = declared_symbols()
     assert decl == set(_lib.EXPORTS)
-    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True,
-                         check=True).stdout
-    exported = set(re.findall(r"\bT (vx_[a-z0-9_]+)", out))
-    missing = decl - exported
-    assert not missing, missing
+    assert dynamic_symbols(_lib.LIB_PATH) == decl
     for name in decl:
         assert hasattr(lib, name)
-    assert lib.vx_abi_version() == 2 == _lib.ABI_VERSION
+    assert lib.vx_abi_version() == 3 == _lib.ABI_VERSION
+    tdecl = declared_symbols(("vx_tuning.h", "vx_synth.h"))
+    assert tdecl == set(_lib.TUNING_EXPORTS) and not tdecl & decl
+    assert dynamic_symbols(_lib.TUNING_PATH) == decl | tdecl
+    assert _lib.tuning().vx_abi_version() == 3
+    assert not any(n.startswith("vx_tuning") for n in dynamic_symbols(_lib.LIB_PATH))
 
 
 def test_no_cpu_fallback_in_product():
@@ -121,12 +153,19 @@ def test_validation_without_gpu(built):
     h = ctypes.c_void_p()
     # option values outside their ranges are refused before any device is looked at
     for field, value in (("zero_copy", 2), ("direct_io", 7), ("verify_ramp", 6), ("batch_chunk", 1000),
-                         ("verify_chunk", 4097), ("verify_cold_chunk", 2048)):
+                         ("verify_chunk", 4097), ("verify_cold_chunk", 2048),
+                         ("verify_chunk", 2 ** 32 - 4096), ("batch_chunk", (1 << 30) + 4096)):
         badopt = _lib.vx_config()
         L.vx_config_default(ctypes.byref(badopt), 262144)
         setattr(badopt, field, value)
         assert L.vx_create(ctypes.byref(badopt), ctypes.byref(h)) == _lib.VX_EINVAL, field
         assert field.encode() in L.vx_last_error() or b"chunk sizes" in L.vx_last_error()
+    # HashPool refuses values a uint32 field would wrap (ctypes does so silently)
+    from vortex_amd.hash_pool import HashPool
+
+    for bad in (-4096, 1 << 32):
+        with pytest.raises(ValueError, match="uint32"):
+            HashPool(262144, verify_chunk=bad)
     if L.vx_device_count() == 0:
         assert L.vx_create(ctypes.byref(cfg), ctypes.byref(h)) == _lib.VX_ENODEV
     bad = _lib.vx_config()
@@ -170,7 +209,7 @@ def test_ragged_plan_host(built):
     pieces, small batches) to the split kernel."""
     from vortex_amd import _lib
 
-    plan = _lib.lib().vx_tuning_plan_ragged
+    plan = _lib.tuning().vx_tuning_plan_ragged
     LANE, SPLIT, WIDE = 1, 2, 5  # WIDE: split, one pair per CU (chain-bound with room to spare)
     KiB, MiB = 1024, 1 << 20
     assert plan(65536, 256 * KiB, 65536 * 256 * KiB) == LANE                     # config 2 as a ragged batch
@@ -188,7 +227,7 @@ def test_zero_copy_plan_host(built):
     three-wave form with a loader wave."""
     from vortex_amd import _lib
 
-    zc = _lib.lib().vx_tuning_zero_copy_plan
+    zc = _lib.tuning().vx_tuning_zero_copy_plan
     KiB, MiB = 1024, 1 << 20
     assert zc(8192, 8192 * 16 * KiB) == 1       # 16 KiB pieces, a full 128 MiB slot
     assert zc(512, 512 * 256 * KiB) == 1        # config 1's 256 KiB pieces
@@ -204,7 +243,7 @@ def _schedule(L, C, head, tail):
 
     from vortex_amd import _lib
 
-    fn = _lib.lib().vx_tuning_chunk_schedule
+    fn = _lib.tuning().vx_tuning_chunk_schedule
     n = fn(L, C, head, tail, None, 0)
     out = (ctypes.c_uint64 * (2 * max(n, 1)))()
     assert fn(L, C, head, tail, out, n) == n
@@ -428,3 +467,74 @@ def test_every_engine_option_is_tested_off_default(built):
         default = getattr(cfg, opt)
         tested = {v for v in vals.get(opt, set()) if isinstance(v, int)}
         assert tested - {default}, f"vx_config.{opt}: no -m gpu test sets a non-default value (seen {tested})"
+
+
+def _split(n, pl, total, threads, rate=2.2e9, g=1):
+    from vortex_amd import _lib
+
+    p = _lib.vx_plan()
+    first, count = ctypes.c_uint64(), ctypes.c_uint64()
+    assert _lib.lib().vx_plan_verify_split(n, pl, total, threads, rate, g, ctypes.byref(first), ctypes.byref(count),
+                                           ctypes.byref(p)) == 0
+    return first.value, count.value, p
+
+
+def test_plan_verify_split_host(built):
+    """vx_plan_verify_split (include/vx_hash.h), host-only: the GPUs take a
+    contiguous tail, the pool the head, and the split's predicted time —
+    the slower side's — never exceeds either side alone; it keeps the pool
+    alone (count 0) when no split beats it by the 10 % margin, e.g. linux-mint
+    on a full 128-thread node, where one 2 MiB chain (~25 ms) outlasts the
+    whole pool (~11 ms)."""
+    MiB = 1 << 20
+    for n, pl, total, t, g in ((1387, 2 * MiB, 2907832320, 16, 1), (11093, 256 * 1024, 11093 * 256 * 1024, 64, 1),
+                               (174, 16 * MiB, 174 * 16 * MiB, 16, 1), (8192, 16 * MiB, 8192 * 16 * MiB, 128, 8),
+                               (65536, 256 * 1024, 65536 * 256 * 1024, 16, 1), (3, 4 * MiB, 3 * 4 * MiB, 16, 1)):
+        first, count, p = _split(n, pl, total, t, g=g)
+        assert first + count == n and 0 <= count <= n
+        alone_cpu = _plan_g(n, pl, total, t, g).cpu_s
+        alone_gpu = _plan_g(n, pl, total, t, g).gpu_s
+        t_split = max(p.gpu_s, p.cpu_s)
+        if count:
+            assert p.use_gpu == 1 and t_split * 1.1 < alone_cpu and t_split <= alone_gpu * 1.0001, (n, pl, t)
+            assert p.gpu_s > 0 and (count == n or p.cpu_s > 0)
+        else:
+            assert p.use_gpu == 0 and p.gpu_s == 0 and p.cpu_s == pytest.approx(alone_cpu)
+    # config 5 on the GPU box's 16 threads: the GPU takes most pieces, and the two sides meet
+    first, count, p = _split(1387, 2 * MiB, 2907832320, 16)
+    assert 800 < count < 1200 and abs(p.gpu_s - p.cpu_s) < 0.15 * max(p.gpu_s, p.cpu_s)
+    # the split's GPU share charges its reads to the pool's cores: fewer pieces than an uncharged model gives
+    assert max(p.gpu_s, p.cpu_s) < 0.8 * _plan_g(1387, 2 * MiB, 2907832320, 16, 1).gpu_s
+    # full node: pool alone
+    assert _split(1387, 2 * MiB, 2907832320, 128, g=8)[1] == 0
+    # one piece and an empty torrent
+    assert _split(1, 2 * MiB, 2 * MiB, 16)[1] == 0 and _split(0, 2 * MiB, 0, 16)[:2] == (0, 0)
+    from vortex_amd import _lib
+    assert _lib.lib().vx_plan_verify_split(10, 0, 10, 16, 2e9, 1, None, None, None) == _lib.VX_EINVAL
+    from vortex_amd.hash_pool import plan_verify_split
+    d = plan_verify_split(1387, 2 * MiB, 2907832320, cpu_threads=16, cpu_thread_rate=2.2e9)
+    assert (d["gpu_first"], d["gpu_count"]) == (first, count) and d["use_gpu"] is True
+
+
+def test_plan_verify_split_on_measured_grid(built):
+    """Against the measured crossover grid (profiles/r02/crossover/grid.json,
+    GPU and CPU-pool times of the same warm files on one box): wherever the
+    split takes part, the two sides' measured rates put through the split's
+    proportions predict a call no slower than the faster side alone."""
+    import json
+
+    grid = json.load(open(os.path.join(ROOT, "profiles", "r02", "crossover", "grid.json")))
+    threads = grid["threads"]
+    seen = 0
+    for pt in grid["points"]:
+        n, L = pt["n"], pt["piece_MiB"] << 20
+        g_s, c_s = pt["gpu_s"], pt["cpu_s"]
+        first, count, p = _split(n, L, n * L, threads, rate=n * L / c_s / threads)
+        if not count:
+            continue
+        seen += 1
+        # measured rates, each side on its share (the GPU side keeps its fixed chain floor)
+        gpu_side = max(g_s * count / n, p.gpu_chain_s)
+        cpu_side = c_s * first / n
+        assert max(gpu_side, cpu_side) <= min(g_s, c_s) * 1.0001, pt
+    assert seen >= 5

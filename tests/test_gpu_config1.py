@@ -56,7 +56,7 @@ def test_config1_async_4096x256k(built, gpu, table):
             got[r.index] = r
         assert pool.pending == 0
         st = pool.stats()
-        zc = _lib.lib().vx_tuning_zero_copy_slots(pool._h)
+        zc = pool.stats()["zero_copy_slots"]
         for b in bufs:
             pool.unregister_buffer(b)
     assert sorted(got) == list(range(N))

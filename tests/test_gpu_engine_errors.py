@@ -50,21 +50,21 @@ def test_batch_failure_part_way_leaves_clean_context(built, gpu, fail_at):
         keep.append(body)
     want = [hashlib.sha1(b).digest() for b in keep]
     # slot_bytes 1 MiB: ~10 pieces per slot, so several slots are in flight when the failure hits
-    with HashPool(plen, slots=3, batch_pieces=8, slot_bytes=1 << 20) as pool:
+    with HashPool(plen, slots=3, batch_pieces=8, slot_bytes=1 << 20, hooks=True) as pool:
         pool.register_buffer(reg)
-        lib().vx_tuning_fail_submit_after(pool._h, fail_at)
+        pool.lib.vx_tuning_fail_submit_after(pool._h, fail_at)
         with pytest.raises(VxError) as e:
             pool.verify_batch(pieces, want)
         assert e.value.code == VX_ENOMEM
         assert pool.pending == 0
         assert pool.try_iter() == []
-        lib().vx_tuning_fail_submit_after(pool._h, -1)
+        pool.lib.vx_tuning_fail_submit_after(pool._h, -1)
         matched, dig = pool.verify_batch(pieces, want)
         assert matched == [True] * n and dig == want
         pool.unregister_buffer(reg)  # nothing in flight: must not be EBUSY
     # the failure also hits the async path without latching the context
-    with HashPool(plen, slots=2, batch_pieces=4) as pool:
-        lib().vx_tuning_fail_submit_after(pool._h, 3)
+    with HashPool(plen, slots=2, batch_pieces=4, hooks=True) as pool:
+        pool.lib.vx_tuning_fail_submit_after(pool._h, 3)
         bufs = [bytearray(keep[i]) for i in range(6)]
         for i in range(3):
             pool.spawn(i, 0, bufs[i], len(bufs[i]), want[i])
@@ -175,9 +175,9 @@ def test_device_failure_recovery(built, gpu):
     for i, b in enumerate(bodies):
         pinned[i * plen:(i + 1) * plen] = b
     digests = [hashlib.sha1(b).digest() for b in bodies]
-    pool = HashPool(plen, slots=3, batch_pieces=8)
+    pool = HashPool(plen, slots=3, batch_pieces=8, hooks=True)
     pool.register_buffer(pinned)
-    lib().vx_tuning_fail_launch_after(pool._h, 2)
+    pool.lib.vx_tuning_fail_launch_after(pool._h, 2)
     results, refused = {}, None
     for i in range(n):
         try:
@@ -235,14 +235,14 @@ def test_submit_ownership_every_tag_once(built, gpu, mode):
     exp = [d if i % 13 else bytes(20) for i, d in enumerate(digests)]  # some planted mismatches
     # slots=2: vx_flush defers its launch while the other slot is in flight, so the
     # failing launch may be vx_poll's lazy one as well as vx_flush's or vx_submit's
-    pool = HashPool(plen, slots=2 if mode == "launch_two_slots" else 3, batch_pieces=8)
+    pool = HashPool(plen, slots=2 if mode == "launch_two_slots" else 3, batch_pieces=8, hooks=True)
     pool.register_buffer(reg)
     if mode == "submit_enomem":
         fails = {5, 6, 30, 71}  # non-sticky: the context stays usable after each
     elif mode == "launch_in_submit":
-        lib().vx_tuning_fail_launch_after(pool._h, 2)
+        pool.lib.vx_tuning_fail_launch_after(pool._h, 2)
     else:
-        lib().vx_tuning_fail_launch_after(pool._h, 3)
+        pool.lib.vx_tuning_fail_launch_after(pool._h, 3)
     seen: dict[int, str] = {}
     dead = False
 
@@ -255,7 +255,7 @@ def test_submit_ownership_every_tag_once(built, gpu, mode):
 
     for i in range(n):
         if mode == "submit_enomem" and i in fails:
-            lib().vx_tuning_fail_submit_after(pool._h, 0)
+            pool.lib.vx_tuning_fail_submit_after(pool._h, 0)
         try:
             pool.spawn(i, 7, bufs[i], plen, exp[i])
         except VxError as e:

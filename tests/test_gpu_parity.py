@@ -776,7 +776,7 @@ def test_api_misuse_and_lifecycle(built, gpu):
     with pytest.raises(VxError) as e:
         pool.spawn(5, 1, bytearray(10), 10)  # row 5 outside a 2-row table
     assert e.value.code == VX_EINVAL
-    L = _lib.lib()
+    L = pool.lib
     assert L.vx_register_host_buffer(pool._h, ctypes.c_void_p(ctypes.addressof(
         ctypes.c_char.from_buffer(buf)) + 100), 10) == VX_EINVAL  # overlaps the registration
     pool.unregister_buffer(buf)
@@ -825,10 +825,10 @@ def test_strided_batch_chunked(built, gpu, L, hs_extra, n, last_len, slot_mib, c
         exp[i] = bytes(20)
     with HashPool(L, slots=3, slot_bytes=slot_mib << 20, **opts) as pool:
         pool.register_buffer(buf)
-        r0 = _lib.lib().vx_tuning_chunk_rounds(pool._h)
+        r0 = pool.stats()["chunk_rounds"]
         dig = pool.sha1_batch(pieces)
         matched, dig2 = pool.verify_batch(pieces, exp)
-        rounds = _lib.lib().vx_tuning_chunk_rounds(pool._h) - r0
+        rounds = pool.stats()["chunk_rounds"] - r0
         pool.unregister_buffer(buf)
     assert dig == want and dig2 == want
     assert matched == [i not in bad for i in range(n)]
@@ -837,7 +837,7 @@ def test_strided_batch_chunked(built, gpu, L, hs_extra, n, last_len, slot_mib, c
     with HashPool(L, slots=3, slot_bytes=slot_mib << 20, batch_chunk=0) as pool:
         pool.register_buffer(buf)
         matched0, dig0 = pool.verify_batch(pieces, exp)
-        assert _lib.lib().vx_tuning_chunk_rounds(pool._h) == 0
+        assert pool.stats()["chunk_rounds"] == 0
         pool.unregister_buffer(buf)
     assert matched0 == matched and dig0 == want
 
@@ -874,7 +874,7 @@ def test_scattered_registered_pieces(built, gpu):
     assert want[3] == oracle.sha1(bytes(allp[3]))
     with HashPool(1 << 21, slots=3, batch_pieces=24, slot_bytes=8 << 20, zero_copy=0) as pool:
         pool.register_buffer(buf)
-        t0 = _lib.lib().vx_tuning_gather_tiles(pool._h)
+        t0 = pool.stats()["gather_tiles"]
         for i, p in enumerate(allp):
             pool.spawn(i, 3, p, len(p), want[i] if i % 9 else bytes(20))
             if i % 10 == 9:
@@ -882,7 +882,7 @@ def test_scattered_registered_pieces(built, gpu):
         pool.drain()
         got = {r.index: (r.hash_matched, r.digest) for r in pool.try_iter()}
         dig = pool.sha1_batch(allp)  # not strided: slot path
-        tiles = _lib.lib().vx_tuning_gather_tiles(pool._h) - t0
+        tiles = pool.stats()["gather_tiles"] - t0
         pool.unregister_buffer(buf)
     assert len(got) == len(allp)
     for i in range(len(allp)):
@@ -949,12 +949,12 @@ def test_gather_batch_chunked(built, gpu, chunk):
     with HashPool(max(lens), slots=3, slot_bytes=4 << 20, **opts) as pool:  # 4 MiB slots: several windows
         for b in bufs:
             pool.register_buffer(b)
-        r0 = _lib.lib().vx_tuning_chunk_rounds(pool._h)
-        t0 = _lib.lib().vx_tuning_gather_tiles(pool._h)
+        r0 = pool.stats()["chunk_rounds"]
+        t0 = pool.stats()["gather_tiles"]
         dig = pool.sha1_batch(pieces)
         matched, dig2 = pool.verify_batch(pieces, exp)
-        rounds = _lib.lib().vx_tuning_chunk_rounds(pool._h) - r0
-        tiles = _lib.lib().vx_tuning_gather_tiles(pool._h) - t0
+        rounds = pool.stats()["chunk_rounds"] - r0
+        tiles = pool.stats()["gather_tiles"] - t0
         for b in bufs:
             pool.unregister_buffer(b)
     assert dig == want and dig2 == want
@@ -964,7 +964,7 @@ def test_gather_batch_chunked(built, gpu, chunk):
     assert tiles == 2 * sum((L + C - 1) // C for L in lens)  # one tile per chunk (C <= 64 KiB)
     with HashPool(max(lens), slots=3, slot_bytes=4 << 20, batch_chunk=0) as pool:
         matched0, dig0 = pool.verify_batch(pieces, exp)  # unregistered: whole-piece staged path
-        assert _lib.lib().vx_tuning_chunk_rounds(pool._h) == 0
+        assert pool.stats()["chunk_rounds"] == 0
     assert matched0 == matched and dig0 == want
 
 
@@ -1043,9 +1043,9 @@ def test_ragged_host_batch_streaming(built, gpu):
     exp = [w if i % 11 else bytes(20) for i, w in enumerate(want)]
     with HashPool(max(lens), slots=3, slot_bytes=4 << 20) as pool:  # 64 lanes per round: lane limit binds
         pool.register_buffer(buf)
-        t0 = _lib.lib().vx_tuning_gather_tiles(pool._h)
+        t0 = pool.stats()["gather_tiles"]
         matched, dig = pool.verify_batch(pieces, exp)
-        tiles = _lib.lib().vx_tuning_gather_tiles(pool._h) - t0
+        tiles = pool.stats()["gather_tiles"] - t0
         dig2 = pool.sha1_batch(pieces)
         pool.unregister_buffer(buf)
         matched_plain, dig_plain = pool.verify_batch([bytes(p) for p in pieces], exp)  # whole-piece slots

@@ -68,12 +68,12 @@ def test_zero_copy_async_ragged_exact(built, gpu, form, batch, flush_every):
     assert want[5] == oracle.sha1(bytes(pieces[5]))
     with HashPool(2 << 20, slots=3, batch_pieces=batch, slot_bytes=16 << 20) as pool:
         pool.register_buffer(buf)
-        z0 = _lib.lib().vx_tuning_zero_copy_slots(pool._h)
-        t0 = _lib.lib().vx_tuning_gather_tiles(pool._h)
+        z0 = pool.stats()["zero_copy_slots"]
+        t0 = pool.stats()["gather_tiles"]
         got = _run_async(pool, pieces, want, flush_every=flush_every)
-        zc = _lib.lib().vx_tuning_zero_copy_slots(pool._h) - z0
-        zl = _lib.lib().vx_tuning_zero_copy_loader_slots(pool._h)
-        tiles = _lib.lib().vx_tuning_gather_tiles(pool._h) - t0
+        zc = pool.stats()["zero_copy_slots"] - z0
+        zl = pool.stats()["zero_copy_loader_slots"]
+        tiles = pool.stats()["gather_tiles"] - t0
         pool.unregister_buffer(buf)
     assert len(got) == len(pieces)
     for i in range(len(pieces)):
@@ -100,11 +100,11 @@ def test_zero_copy_piece_table_and_batch(built, gpu, batch):
     with HashPool(1 << 16, slots=4, batch_pieces=batch) as pool:
         pool.register_buffer(buf)
         pool.set_piece_table(bytes(table))
-        z0 = _lib.lib().vx_tuning_zero_copy_slots(pool._h)
+        z0 = pool.stats()["zero_copy_slots"]
         got = _run_async(pool, pieces, want, table=True, flush_every=17 if batch == 64 else 1000)
-        z1 = _lib.lib().vx_tuning_zero_copy_slots(pool._h)
+        z1 = pool.stats()["zero_copy_slots"]
         dig = pool.sha1_batch(pieces)
-        zc = _lib.lib().vx_tuning_zero_copy_slots(pool._h) - z0
+        zc = pool.stats()["zero_copy_slots"] - z0
         pool.unregister_buffer(buf)
     for i in range(len(pieces)):
         assert got[i] == (i % 13 != 0, want[i]), i
@@ -126,9 +126,9 @@ def test_zero_copy_mixed_slots_fall_back(built, gpu):
     want = [hashlib.sha1(p).digest() for p in allp]
     with HashPool(2 << 20, slots=3, batch_pieces=24, slot_bytes=16 << 20) as pool:
         pool.register_buffer(buf)
-        t0 = _lib.lib().vx_tuning_gather_tiles(pool._h)
+        t0 = pool.stats()["gather_tiles"]
         got = _run_async(pool, allp, want)
-        tiles = _lib.lib().vx_tuning_gather_tiles(pool._h) - t0
+        tiles = pool.stats()["gather_tiles"] - t0
         pool.unregister_buffer(buf)
     for i in range(len(allp)):
         assert got[i] == (i % 9 != 0, want[i]), i
@@ -154,14 +154,14 @@ def test_zero_copy_config1_shape(built, gpu):
     with HashPool(plen) as pool:
         for m in bufs:
             pool.register_buffer(m)
-        z0 = _lib.lib().vx_tuning_zero_copy_slots(pool._h)
+        z0 = pool.stats()["zero_copy_slots"]
         for k, i in enumerate(order):
             pool.spawn(i, 1, bufs[i], plen, clean[20 * i:20 * i + 20])
             if k % 64 == 63:
                 pool.flush()
         pool.drain()
         got = {r.index: (r.hash_matched, r.digest) for r in pool.try_iter()}
-        zc = _lib.lib().vx_tuning_zero_copy_slots(pool._h) - z0
+        zc = pool.stats()["zero_copy_slots"] - z0
         for m in bufs:
             pool.unregister_buffer(m)
     want = oracle.pool_digest_synth(seed, 0, n, plen, corrupt_every=every, threads=8)
@@ -190,7 +190,7 @@ def test_zero_copy_default_policy(built, gpu, plen, batch, zero_copy):
                   zero_copy=zero_copy) as pool:
         pool.register_buffer(buf)
         got = _run_async(pool, pieces, want, flush_every=batch)
-        zc = _lib.lib().vx_tuning_zero_copy_slots(pool._h)
+        zc = pool.stats()["zero_copy_slots"]
         st = pool.stats()
         pool.unregister_buffer(buf)
     for i in range(n):

@@ -18,7 +18,7 @@ RUST_TO_C = {
     "u8": "uint8_t", "u32": "uint32_t", "u64": "uint64_t", "i32": "int32_t", "i64": "int64_t",
     "usize": "size_t", "c_int": "int", "c_char": "char", "c_void": "void", "f64": "double",
     "VxCtx": "vx_ctx", "VxConfig": "vx_config", "VxCompletion": "vx_completion", "VxPlan": "vx_plan",
-    "VxStats": "vx_stats",
+    "VxStats": "vx_stats", "VxVerifyTrace": "vx_verify_trace", "VxVerifyRound": "vx_verify_round",
 }
 
 
@@ -140,7 +140,8 @@ def test_rust_externs_match_header():
 def test_rust_structs_match_header():
     c = c_structs()
     r = rust_structs()
-    pairs = {"VxCompletion": "vx_completion", "VxConfig": "vx_config", "VxPlan": "vx_plan"}
+    pairs = {"VxCompletion": "vx_completion", "VxConfig": "vx_config", "VxPlan": "vx_plan", "VxStats": "vx_stats",
+             "VxVerifyTrace": "vx_verify_trace", "VxVerifyRound": "vx_verify_round"}
     for rname, cname in pairs.items():
         assert r[rname] == c[cname], f"{rname} vs {cname}: {r[rname]} / {c[cname]}"
     assert r["VxCtx"] == [("_private", "uint8_t[0]")]  # opaque handle

@@ -168,6 +168,24 @@ def test_direct_reads_of_uncached_ranges(tmp_path):
         half = run(1, evict="half")
         assert 0.3 < resident[-1] < 0.9, resident
         assert 0 < half < cold
+        # a small file of a large torrent, its first 80 % cached: with 2 residency samples
+        # (both in the cached part) it looked all cached and nothing went direct; with the per-file
+        # minimum it is probed per read, so the uncached tail's aligned ranges go O_DIRECT
+        big = path + ".big"
+        with open(big, "wb") as f:
+            f.truncate(1 << 30)  # sparse: only its share of the samples matters
+        try:
+            fd = os.open(path, os.O_RDONLY)
+            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_DONTNEED)
+            os.posix_fadvise(fd, 0, 0, os.POSIX_FADV_RANDOM)
+            os.pread(fd, int((8 << 20) * 0.8) & ~4095, 0)
+            os.close(fd)
+            out = subprocess.run([str(exe), path, "2", big], capture_output=True, text=True, check=True, timeout=60)
+            res = json.loads(out.stdout)
+            assert res["reads"] >= 9 and res["mismatches"] == 0, res
+            assert res["direct_bytes"] > 0, res
+        finally:
+            os.unlink(big)
         # another file renamed over the path after the open: reads still match the opened file
         other = path + ".new"
         with open(other, "wb") as f:

@@ -34,7 +34,7 @@ def main() -> None:
     import torch
 
     from vortex_amd import device as vdev
-    from vortex_amd._lib import check, lib
+    from vortex_amd._lib import check, tuning
 
     hip = ctypes.CDLL("libamdhip64.so")
     hip.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_uint]
@@ -62,7 +62,7 @@ def main() -> None:
                 vdev.sha1_ragged(hbm, offs, lens, digests=digs[kind], variant=2, validate=False)
             else:
                 srcs = src_hbm if kind == "zc_hbm" else src_host
-                check(lib().vx_tuning_zero_copy_kernel(srcs.data_ptr(), lens.data_ptr(), n, digs[kind].data_ptr(),
+                check(tuning().vx_tuning_zero_copy_kernel(srcs.data_ptr(), lens.data_ptr(), n, digs[kind].data_ptr(),
                                                        None, None, a.loader, int(st.cuda_stream)), "zc kernel")
 
         res = {"pieces": n, "piece_len": plen}

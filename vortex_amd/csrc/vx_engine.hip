@@ -156,7 +156,6 @@ struct vx_ctx {
     // +57 % and +7 % on two boxes but -2 % and -5 % (median of 6 and 10
     // evicted calls) on two more, 512 KiB +4 % (profiles/r03/cold/): the
     // box's disk decides, not the chunk.
-    uint64_t chunk_rounds = 0;  // chunk rounds launched (vx_tuning_chunk_rounds)
     // Per-piece device rows of the chunk paths (state | expected | digest |
     // verdict), kept across calls and grown on demand: allocating them per
     // call cost ~1 ms of a 40 ms e2e batch.
@@ -185,28 +184,32 @@ struct vx_ctx {
     // A slot whose pieces are all registered and aligned is hashed straight
     // out of host memory by the zero-copy kernel, without a gather
     // (sha1_zc_split_kernel), unless cfg.zero_copy is 0.
-    uint64_t zero_copy_slots = 0;         // slots hashed that way (vx_tuning_zero_copy_slots)
-    uint64_t zero_copy_loader_slots = 0;  // ... of them in the three-wave form (zc_loader_wins)
-    uint64_t gather_tiles = 0;  // tiles gathered (vx_tuning_gather_tiles)
+    // (counted in vx_stats.zero_copy_slots / zero_copy_loader_slots)
     uint64_t pending = 0;
     uint64_t seq = 0;
     int sticky = 0;
-    // Fault injection for tests (vx_tuning_fail_submit_after): the submit
-    // after this many more succeeds fails with VX_ENOMEM, the way a failed
-    // pinned-stage allocation does; < 0 = off.
+#ifdef VX_TEST_HOOKS
+    // Fault injection, only in the test build libvortex_amd_tuning.so
+    // (vx_tuning_fail_submit_after): the submit after this many more succeeds
+    // fails with VX_ENOMEM, the way a failed pinned-stage allocation does;
+    // < 0 = off.
     int64_t fail_submit_after = -1;
     // vx_tuning_fail_launch_after: the launch after this many more fails as a
     // device error would, turning the context sticky; < 0 = off.
     int64_t fail_launch_after = -1;
+#endif
     vx_stats stats{};  // vx_get_stats (observability counters)
     // harvest() counts mismatches unless the caller overrides verdicts after
     // it (the file re-verify: a piece with an I/O error is counted in
     // io_errors only, FileVerify::consume counts the final verdicts)
     bool harvest_counts_mismatches = true;
-    // vx_tuning_last_verify: the last file re-verify's time budget, and the
-    // timing events around its chunk rounds' data copies (reused across calls)
+    // vx_last_verify: the last file re-verify's time budget, and the timing
+    // events around its chunk rounds' data copies (reused across calls)
     vx_verify_trace last_verify{};
     std::vector<hipEvent_t> copy_ev;
+    std::vector<vx_verify_round> last_rounds;  // vx_last_verify_rounds
+    hipEvent_t anchor_ev = nullptr;            // maps the rounds' GPU times onto the host clock
+    uint64_t verify_t0_ns = 0;                 // the running re-verify call's start (steady clock)
 };
 
 namespace {
@@ -440,8 +443,10 @@ int warm_slots(vx_ctx* c) {
 // A failed launch leaves a slot half-enqueued: the context turns sticky and
 // every later call reports the error (vx_destroy still cleans up).
 int launch_slot(vx_ctx* c, int si) {
+#ifdef VX_TEST_HOOKS
     if (c->fail_launch_after >= 0 && c->fail_launch_after-- == 0)
         return c->sticky = fail(VX_EDEVICE, "launch: injected device failure (vx_tuning_fail_launch_after)");
+#endif
     const int rc = launch_slot_impl(c, si);
     if (rc) c->sticky = rc;
     return rc;
@@ -504,7 +509,6 @@ int launch_slot_impl(vx_ctx* c, int si) {
         const uint32_t grid = s.bytes >= (uint64_t)n << 21 ? 128u : 0u;
         hipError_t e = vx::launch_gather(s.d_src, s.d_offsets, s.d_lens, s.d_tfirst, n, s.gtiles, s.d_arena, cs, grid);
         if (e != hipSuccess) return hip_fail(e, "gather launch");
-        c->gather_tiles += s.gtiles;
         c->stats.gather_tiles += s.gtiles;
     }
     if (s.use_table)
@@ -519,8 +523,8 @@ int launch_slot_impl(vx_ctx* c, int si) {
     if (zc) {
         const bool loader = zc_loader_wins(n);
         e = vx::launch_zero_copy(s.d_src, s.d_lens, n, s.d_digests, d_exp, s.d_matched, loader, s.stream, d_row);
-        c->zero_copy_slots++;
-        c->zero_copy_loader_slots += loader;
+        c->stats.zero_copy_slots++;
+        c->stats.zero_copy_loader_slots += loader;
     } else if (s.uniform) {
         const uint32_t len = s.h_lens[0];
         const uint64_t stride = align_up(std::max<uint32_t>(len, 1), kAlign);
@@ -636,8 +640,10 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
     if (c->sticky) return c->sticky;
     if (!data && len) return fail(VX_EINVAL, "vx_submit: data is NULL");
     if (len > c->cfg.max_piece_len) return fail(VX_ERANGE, "vx_submit: piece longer than max_piece_len");
+#ifdef VX_TEST_HOOKS
     if (c->fail_submit_after >= 0 && c->fail_submit_after-- == 0)
         return fail(VX_ENOMEM, "vx_submit: injected failure (vx_tuning_fail_submit_after)");
+#endif
     const bool table = piece_row >= 0;
     int si = acquire_filling(c);
     if (si < 0) return si;
@@ -797,6 +803,12 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
         (cfg->verify_chunk && (cfg->verify_chunk < 4096 || cfg->verify_chunk % 4096)) ||
         (cfg->verify_cold_chunk && (cfg->verify_cold_chunk < 4096 || cfg->verify_cold_chunk % 4096)))
         return fail(VX_EINVAL, "vx_create: chunk sizes must be 0 or multiples of 4096");
+    // At most 1 GiB: a wrapped negative value from a binding is a huge
+    // multiple of 4096.  (A chunk larger than a slot's arena is
+    // legal: those calls take the whole-piece path.)
+    constexpr uint32_t kMaxChunk = 1u << 30;
+    if (cfg->batch_chunk > kMaxChunk || cfg->verify_chunk > kMaxChunk || cfg->verify_cold_chunk > kMaxChunk)
+        return fail(VX_EINVAL, "vx_create: chunk sizes must be at most 1 GiB");
     const int ndev = vx_device_count();
     if (cfg->device < 0 || cfg->device >= ndev) return fail(VX_ENODEV, "vx_create: no such HIP device");
     vx_ctx* c = new (std::nothrow) vx_ctx();
@@ -837,6 +849,7 @@ int vx_destroy(vx_ctx* c) {
     if (c->chunk_prev) (void)hipEventDestroy(c->chunk_prev);
     for (hipEvent_t e : c->copy_ev)
         if (e) (void)hipEventDestroy(e);
+    if (c->anchor_ev) (void)hipEventDestroy(c->anchor_ev);
     delete c;
     return rc;
 }
@@ -1247,7 +1260,6 @@ struct ChunkPipe {
         if (!rc && (hipEventRecord(prev_kernel, st) != hipSuccess || hipEventRecord(s.done, st) != hipSuccess))
             rc = fail(VX_EDEVICE, "chunk round: event record failed");
         have_prev = true;
-        c->chunk_rounds++;
         c->stats.chunk_rounds++;
         s.state = Slot::INFLIGHT;
         s.seq = c->seq++;
@@ -1352,6 +1364,8 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
         int si;
         uint32_t m;
         uint64_t ticket, bytes;
+        uint32_t flags;          // VX_ROUND_* (the round timeline)
+        uint64_t t_submit = 0;   // its reads queued (steady-clock ns)
     };
     std::vector<Round> rounds;
     for (uint64_t w0 = first; w0 < end; w0 += W) {
@@ -1359,8 +1373,13 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
         const uint64_t wmax = w1 == n ? std::max<uint64_t>(pl, last_len) : pl;
         const int ramp = (int)c->cfg.verify_ramp;
         const auto sched = chunk_schedule(wmax, C, w0 == first ? ramp : 0, w1 == end ? ramp : 0);
-        for (size_t k = 0; k < sched.size(); ++k)
-            rounds.push_back(Round{w0, w1, sched[k].first, sched[k].second, k > 0, -1, 0, 0, 0});
+        for (size_t k = 0; k < sched.size(); ++k) {
+            const uint64_t a = sched[k].first, len = sched[k].second;
+            const uint32_t fl = (k == 0 ? VX_ROUND_NEW_WINDOW : 0u) |
+                                (len < C && a < C && w0 == first ? VX_ROUND_HEAD_RAMP : 0u) |
+                                (len < C && a >= C && w1 == end ? VX_ROUND_TAIL_RAMP : 0u);
+            rounds.push_back(Round{w0, w1, a, len, k > 0, -1, 0, 0, 0, fl});
+        }
     }
     const size_t nslots = c->slots.size();
     const size_t depth = nslots > 1 ? std::min<size_t>(kReadahead, nslots - 1) : 0;
@@ -1369,10 +1388,21 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     auto ms = [](clk::time_point a, clk::time_point b) {
         return std::chrono::duration<double, std::milli>(b - a).count();
     };
-    // A (start, end) timing-event pair around each round's data copy, kept on
-    // the context and reused (vx_tuning_last_verify).
+    // Timing events around each round's data copy and after its kernel
+    // (start, end, kernel end), kept on the context and reused
+    // (vx_last_verify / vx_last_verify_rounds).  An anchor event recorded on
+    // an idle stream now maps GPU times onto the host clock of the call.
     size_t timed = 0;
     std::vector<uint64_t> timed_bytes;
+    std::vector<vx_verify_round> tl;  // the round timeline, one per enqueued round
+    std::vector<long> tl_ev;          // timed-copy index of each timeline round, -1 when untimed
+    bool anchored = false;
+    uint64_t t_anchor = 0;
+    if (c->anchor_ev || hipEventCreate(&c->anchor_ev) == hipSuccess) {
+        anchored = hipEventRecord(c->anchor_ev, c->slots[0].stream) == hipSuccess;
+        t_anchor = vx_files::Readers::now_ns();
+    }
+    auto rel_ms = [&](uint64_t t_ns) { return t_ns ? ((double)t_ns - (double)c->verify_t0_ns) * 1e-6 : 0.0; };
     auto t_last_enqueue = clk::now();
     auto consume = [&] { fv.consume(); };
     // Reserve a slot for round r and queue its reads; false when no slot is
@@ -1411,6 +1441,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
         s.state = Slot::FILLING;  // reserved until the round is enqueued
         s.bytes = r.bytes = (uint64_t)(m - 1) * pitch + s.h_lens[m - 1];
         r.si = si;
+        r.t_submit = vx_files::Readers::now_ns();
         r.ticket = rd.submit(it);
         return true;
     };
@@ -1421,22 +1452,36 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
         Round& r = rounds[ne];
         if (r.m == 0) continue;
         rd.wait(r.ticket);
+        vx_verify_round vr{};
+        vr.read_submit_ms = rel_ms(r.t_submit);
+        vr.read_done_ms = rel_ms(rd.done_ns(r.ticket));
+        vr.enqueue_ms = rel_ms(vx_files::Readers::now_ns());
+        vr.bytes = r.bytes;
+        vr.offset = r.a;
+        vr.lanes = r.m;
+        vr.flags = r.flags;
+        long ev_k = -1;
         rc = cp.round(r.si, r.m, r.continues, false, [&](Slot& sl, hipStream_t st) {
             bool ev = true;
-            while (ev && c->copy_ev.size() < 2 * timed + 2) {
+            while (ev && c->copy_ev.size() < 3 * timed + 3) {
                 hipEvent_t e = nullptr;
                 ev = hipEventCreate(&e) == hipSuccess;
                 if (ev) c->copy_ev.push_back(e);
             }
-            ev = ev && hipEventRecord(c->copy_ev[2 * timed], st) == hipSuccess;
+            ev = ev && hipEventRecord(c->copy_ev[3 * timed], st) == hipSuccess;
             if (hipMemcpyAsync(sl.d_arena, sl.h_stage, sl.bytes, hipMemcpyHostToDevice, st) != hipSuccess)
                 return fail(VX_EDEVICE, "vx_verify_files: chunk H2D failed");
-            if (ev && hipEventRecord(c->copy_ev[2 * timed + 1], st) == hipSuccess) {  // timing is best effort
+            if (ev && hipEventRecord(c->copy_ev[3 * timed + 1], st) == hipSuccess) {  // timing is best effort
                 timed_bytes.push_back(sl.bytes);
-                ++timed;
+                ev_k = (long)timed++;
             }
             return 0;
         });
+        // after the round's chunk kernel (cp.round enqueued it on the slot's stream)
+        if (!rc && ev_k >= 0 && hipEventRecord(c->copy_ev[3 * ev_k + 2], c->slots[r.si].stream) != hipSuccess)
+            ev_k = -1;
+        tl.push_back(vr);
+        tl_ev.push_back(ev_k);
         t_last_enqueue = clk::now();
     }
     rd.wait();  // error path: no read may still target a stage
@@ -1451,15 +1496,26 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     if (!rc && timed) {  // finish() waited for every round: the copy events are complete
         float a = 0, b = 0, busy = 0;
         for (size_t k = 0; k < timed; ++k) {
-            (void)hipEventElapsedTime(&a, c->copy_ev[0], c->copy_ev[2 * k]);
-            (void)hipEventElapsedTime(&b, c->copy_ev[0], c->copy_ev[2 * k + 1]);
+            (void)hipEventElapsedTime(&a, c->copy_ev[0], c->copy_ev[3 * k]);
+            (void)hipEventElapsedTime(&b, c->copy_ev[0], c->copy_ev[3 * k + 1]);
             busy += b - a;
             vt.copy_bytes += timed_bytes[k];
         }
         vt.copy_busy_ms = busy;
         vt.copy_span_ms = b;
         vt.rounds = (uint32_t)timed;
+        // GPU times on the call's host clock, through the anchor
+        const double base = anchored ? ((double)t_anchor - (double)c->verify_t0_ns) * 1e-6 : 0.0;
+        for (size_t k = 0; k < tl.size() && anchored; ++k) {
+            if (tl_ev[k] < 0) continue;
+            float x = 0;
+            const size_t e = 3 * (size_t)tl_ev[k];
+            if (hipEventElapsedTime(&x, c->anchor_ev, c->copy_ev[e]) == hipSuccess) tl[k].copy_start_ms = base + x;
+            if (hipEventElapsedTime(&x, c->anchor_ev, c->copy_ev[e + 1]) == hipSuccess) tl[k].copy_end_ms = base + x;
+            if (hipEventElapsedTime(&x, c->anchor_ev, c->copy_ev[e + 2]) == hipSuccess) tl[k].kernel_end_ms = base + x;
+        }
     }
+    c->last_rounds = std::move(tl);
     if (!rc)
         for (uint64_t i = 0; i < cnt; ++i)
             if (fv.bad[i]) fv.matched_out[i] = 0;
@@ -1590,7 +1646,6 @@ int batch_chunked_gather(vx_ctx* c, const uint32_t* lens, const uint8_t* expecte
                 return fail(VX_EDEVICE, "batch: gather table H2D failed");
             hipError_t e = vx::launch_gather(sl.d_src, sl.d_offsets, sl.d_lens, sl.d_tfirst, m, tiles, sl.d_arena, st);
             if (e != hipSuccess) return hip_fail(e, "batch: gather launch");
-            c->gather_tiles += tiles;
             c->stats.gather_tiles += tiles;
             return 0;
         };
@@ -1773,6 +1828,8 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
     const uint64_t end = first + count;
     const uint64_t t_call = vx_files::Readers::now_ns();
     c->last_verify = vx_verify_trace{};
+    c->last_rounds.clear();
+    c->verify_t0_ns = t_call;
     const std::vector<vx_files::FileSpan> fs = vx_files::layout(file_lengths, nfiles, piece_length);
     std::vector<int> fds(nfiles, -1);
     for (size_t f = 0; f < nfiles; ++f) fds[f] = open(paths[f], O_RDONLY | O_CLOEXEC);
@@ -1975,27 +2032,86 @@ int vx_plan_verify(uint64_t n_pieces, uint32_t piece_length, uint64_t total_leng
 // term divides by n_gpus; one piece's chain does not shrink, which is why a
 // host with many cores can keep its pool against any number of GPUs when the
 // pieces are long (INTEGRATION.md "A whole node is a different host").
+namespace {
+constexpr double kChainBlock = 0.76e-6, kPcieRate = 52.0 * (1ull << 30), kSetup = 1.5e-3;
+constexpr double kOverlapLoss = 0.08, kMargin = 1.1;
+constexpr double kBatchLatency = 1e-3;  // launch, H2D of a small batch, D2H, poll
+// One reader thread's pread rate from the page cache (a memcpy out of the
+// cache; 7.4-7.8 GiB/s measured per reader, BENCH_r04 reverify.gpu_traces):
+// the host CPU time the GPU side of a split takes from the caller's pool.
+constexpr double kReadRate = 8.0e9;
+
+// The GPU path over `bytes` bytes of pieces piece_length long, over n_gpus links.
+void plan_gpu(double L, double bytes, uint32_t n_gpus, vx_plan* out) {
+    out->gpu_chain_s = std::ceil((L + 9) / 64) * kChainBlock;
+    out->gpu_transfer_s = bytes / kPcieRate / std::max<uint32_t>(1, n_gpus);
+    out->gpu_s = std::max(out->gpu_transfer_s, out->gpu_chain_s) + kSetup +
+                 kOverlapLoss * std::min(out->gpu_transfer_s, out->gpu_chain_s);
+}
+}  // namespace
+
 int vx_plan_verify_gpus(uint64_t n_pieces, uint32_t piece_length, uint64_t total_length, uint32_t cpu_threads,
                         double cpu_thread_rate, uint32_t n_gpus, vx_plan* out) {
     if (!out || piece_length == 0) return fail(VX_EINVAL, "vx_plan_verify: bad argument");
     if (n_pieces != (total_length + piece_length - 1) / piece_length)
         return fail(VX_EINVAL, "vx_plan_verify: n_pieces does not match total_length");
-    constexpr double kChainBlock = 0.76e-6, kPcieRate = 52.0 * (1ull << 30), kSetup = 1.5e-3;
-    constexpr double kOverlapLoss = 0.08, kMargin = 1.1;
-    constexpr double kBatchLatency = 1e-3;  // launch, H2D of a small batch, D2H, poll
     const double threads = cpu_threads ? cpu_threads : 16;
     const double rate = cpu_thread_rate > 0 ? cpu_thread_rate : 2.2e9;
-    const double L = piece_length, blocks = std::ceil((L + 9) / 64);
+    const double L = piece_length;
     *out = vx_plan{};
     if (n_pieces == 0) return 0;
-    out->gpu_chain_s = blocks * kChainBlock;
-    out->gpu_transfer_s = (double)total_length / kPcieRate / std::max<uint32_t>(1, n_gpus);
-    out->gpu_s = std::max(out->gpu_transfer_s, out->gpu_chain_s) + kSetup +
-                 kOverlapLoss * std::min(out->gpu_transfer_s, out->gpu_chain_s);
+    plan_gpu(L, (double)total_length, n_gpus, out);
     out->cpu_s = std::ceil((double)n_pieces / threads) * (L / rate);
     out->piece_latency_s = out->gpu_chain_s + kBatchLatency;
     out->cpu_piece_latency_s = L / rate;
     out->use_gpu = out->gpu_s * kMargin < out->cpu_s ? 1 : 0;
+    return 0;
+}
+
+// The split of one bulk verify between the GPUs (the tail of the piece range)
+// and the caller's pool (the head), run at once: the GPU side's time is the
+// model above over its bytes; the pool's is its pieces plus the GPU side's
+// reads, which run on the same host cores (one reader byte costs
+// rate / kReadRate of a hashed byte), in rounds of one piece per thread.
+// Every split k = 0..n is scored by the slower side and the fastest wins;
+// unless it beats the pool alone by kMargin the pool keeps everything.
+int vx_plan_verify_split(uint64_t n_pieces, uint32_t piece_length, uint64_t total_length, uint32_t cpu_threads,
+                         double cpu_thread_rate, uint32_t n_gpus, uint64_t* gpu_first, uint64_t* gpu_count,
+                         vx_plan* out) {
+    if (!gpu_first || !gpu_count || piece_length == 0) return fail(VX_EINVAL, "vx_plan_verify_split: bad argument");
+    if (n_pieces != (total_length + piece_length - 1) / piece_length)
+        return fail(VX_EINVAL, "vx_plan_verify_split: n_pieces does not match total_length");
+    const double threads = cpu_threads ? cpu_threads : 16;
+    const double rate = cpu_thread_rate > 0 ? cpu_thread_rate : 2.2e9;
+    const double L = piece_length;
+    const double last = n_pieces ? (double)(total_length - (n_pieces - 1) * (uint64_t)piece_length) : 0.0;
+    auto gpu_bytes = [&](uint64_t k) { return k ? (double)(k - 1) * L + last : 0.0; };
+    auto cpu_time = [&](uint64_t k) {  // the pool's n - k pieces plus the GPU side's reads
+        const double work = (double)(n_pieces - k) + gpu_bytes(k) / L * (rate / kReadRate);
+        return work > 0 ? std::ceil(work / threads - 1e-9) * (L / rate) : 0.0;
+    };
+    vx_plan g{};
+    uint64_t best_k = 0;
+    double best_t = cpu_time(0);
+    const double pool_alone = best_t;
+    for (uint64_t k = 1; k <= n_pieces; ++k) {
+        plan_gpu(L, gpu_bytes(k), n_gpus, &g);
+        const double t = std::max(g.gpu_s, cpu_time(k));
+        if (t < best_t) best_t = t, best_k = k;
+    }
+    if (best_k && best_t * kMargin >= pool_alone) best_k = 0;
+    *gpu_count = best_k;
+    *gpu_first = n_pieces - best_k;
+    if (out) {
+        *out = vx_plan{};
+        if (best_k) plan_gpu(L, gpu_bytes(best_k), n_gpus, out);
+        out->cpu_s = cpu_time(best_k);
+        vx_plan one{};
+        plan_gpu(L, L, 1, &one);  // the download path's figures do not depend on the split
+        out->piece_latency_s = one.gpu_chain_s + kBatchLatency;
+        out->cpu_piece_latency_s = L / rate;
+        out->use_gpu = best_k ? 1 : 0;
+    }
     return 0;
 }
 
@@ -2011,11 +2127,18 @@ int vx_reset_stats(vx_ctx* c) {
     return 0;
 }
 
-uint64_t vx_tuning_chunk_rounds(const vx_ctx* c) { return c ? c->chunk_rounds : 0; }
-uint64_t vx_tuning_gather_tiles(const vx_ctx* c) { return c ? c->gather_tiles : 0; }
+int vx_last_verify(const vx_ctx* c, vx_verify_trace* out) {
+    if (!c || !out) return fail(VX_EINVAL, "vx_last_verify: NULL argument");
+    *out = c->last_verify;
+    return 0;
+}
 
-uint64_t vx_tuning_zero_copy_slots(const vx_ctx* c) { return c ? c->zero_copy_slots : 0; }
-uint64_t vx_tuning_zero_copy_loader_slots(const vx_ctx* c) { return c ? c->zero_copy_loader_slots : 0; }
+int64_t vx_last_verify_rounds(const vx_ctx* c, vx_verify_round* out, size_t max) {
+    if (!c || (max && !out)) return fail(VX_EINVAL, "vx_last_verify_rounds: NULL argument");
+    const size_t k = std::min(max, c->last_rounds.size());
+    if (k) std::memcpy(out, c->last_rounds.data(), k * sizeof(vx_verify_round));
+    return (int64_t)c->last_rounds.size();
+}
 
 int vx_tuning_zero_copy_plan(uint32_t n, uint64_t total_len) {
     (void)total_len;  // the policy no longer depends on the slot's bytes (kept in the signature)
@@ -2032,17 +2155,14 @@ int vx_tuning_zero_copy_kernel(const uint64_t* d_srcs, const uint32_t* d_lens, u
                                         loader != 0, static_cast<hipStream_t>(stream));
     return e == hipSuccess ? 0 : hip_fail(e, "vx_tuning_zero_copy_kernel");
 }
-int vx_tuning_last_verify(const vx_ctx* c, vx_verify_trace* out) {
-    if (!c || !out) return fail(VX_EINVAL, "vx_tuning_last_verify: NULL argument");
-    *out = c->last_verify;
-    return 0;
-}
+#ifdef VX_TEST_HOOKS
 void vx_tuning_fail_submit_after(vx_ctx* c, int64_t k) {
     if (c) c->fail_submit_after = k < 0 ? -1 : k;
 }
 void vx_tuning_fail_launch_after(vx_ctx* c, int64_t k) {
     if (c) c->fail_launch_after = k < 0 ? -1 : k;
 }
+#endif
 size_t vx_tuning_chunk_schedule(uint64_t L, uint64_t C, int head, int tail, uint64_t* out, size_t max) {
     if (C < 4 || C % 4) return 0;
     const auto r = chunk_schedule(L, C, std::max(0, std::min(5, head)), std::max(0, std::min(5, tail)));

@@ -148,6 +148,10 @@ class DirectIo {
     static constexpr uint64_t kMinFile = 1ull << 20;
     static constexpr size_t kMaxFiles = 4096;
     static constexpr uint64_t kSamples = 256;  // residency samples per call
+    // ... but at least this many per file (all pages of a smaller one): with
+    // 2 samples a small file of a large torrent, 80 % cached, looked all
+    // cached and was read buffered throughout
+    static constexpr uint64_t kMinSamples = 16;
     static constexpr double kWarm = 0.9;       // a file this cached is read buffered throughout
     static constexpr double kCold = 0.1;       // one this uncached goes O_DIRECT where aligned, unprobed
     // enabled = false: every read is buffered (vx_config.direct_io = 0).
@@ -177,8 +181,9 @@ class DirectIo {
             ++used;
         }
         // Residency, sampled once: about kSamples pages spread over the mapped
-        // files by size (mid-points of equal parts, at least 2 per file, so a
-        // torrent of kMaxFiles files costs ~8,000 mincore calls, not 65,000).
+        // files by size (mid-points of equal parts, at least kMinSamples per
+        // file, so a torrent of kMaxFiles files costs ~64,000 mincore calls,
+        // a few ms).
         uint64_t total = 0;
         for (size_t f = 0; f < map_.size(); ++f)
             if (map_[f]) total += size_[f];
@@ -186,7 +191,7 @@ class DirectIo {
         for (size_t f = 0; f < map_.size() && total; ++f) {
             if (!map_[f]) continue;
             const uint64_t pages = (size_[f] + kBlock - 1) / kBlock;
-            const uint64_t k = std::min<uint64_t>(pages, std::max<uint64_t>(2, kSamples * size_[f] / total));
+            const uint64_t k = std::min<uint64_t>(pages, std::max<uint64_t>(kMinSamples, kSamples * size_[f] / total));
             uint64_t hit = 0;
             for (uint64_t i = 0; i < k; ++i)
                 hit += resident((uint32_t)f, (int64_t)(((2 * i + 1) * pages / (2 * k)) * kBlock)) ? 1 : 0;
@@ -354,6 +359,7 @@ class Readers {
         std::unique_lock<std::mutex> g(mu_);
         const uint64_t id = base_ + jobs_.size();
         jobs_.push_back(Job{&items, 0, items.size()});
+        done_ns_.push_back(0);
         if (inline_) {
             g.unlock();
             std::vector<Seg> segs;
@@ -361,10 +367,14 @@ class Readers {
             g.lock();
             jobs_[id - base_].left = 0;
             jobs_[id - base_].next = items.size();
+            done_ns_[id] = now_ns();
             retire();
             return id;
         }
-        if (items.empty()) retire();
+        if (items.empty()) {
+            done_ns_[id] = now_ns();
+            retire();
+        }
         g.unlock();
         cv_.notify_all();
         return id;
@@ -380,6 +390,11 @@ class Readers {
         done_cv_.wait(g, [&] { return jobs_.empty(); });
     }
     void run(const std::vector<ReadItem>& items) { wait(submit(items)); }
+    // When job `ticket`'s last item finished (steady-clock ns; 0 while unread).
+    uint64_t done_ns(uint64_t ticket) {
+        std::lock_guard<std::mutex> g(mu_);
+        return ticket < done_ns_.size() ? done_ns_[ticket] : 0;
+    }
     // Read accounting (vx_tuning_last_verify): pread time summed over threads,
     // bytes, and the first read's start / the last read's end (steady-clock ns).
     uint64_t busy_ns() const { return busy_ns_.load(std::memory_order_relaxed); }
@@ -464,7 +479,10 @@ class Readers {
             g.unlock();
             (void)read_item(it, segs);
             g.lock();
-            if (--jobs_[id - base_].left == 0) retire();  // the job cannot have retired: left was > 0
+            if (--jobs_[id - base_].left == 0) {  // the job cannot have retired: left was > 0
+                done_ns_[id] = now_ns();
+                retire();
+            }
         }
     }
 
@@ -479,6 +497,7 @@ class Readers {
     std::condition_variable cv_, done_cv_;
     bool stop_ = false, inline_ = false;
     std::deque<Job> jobs_;
+    std::vector<uint64_t> done_ns_;  // per ticket: when its reads finished (the re-verify's round timeline)
     uint64_t base_ = 0;  // id of jobs_.front()
     std::atomic<uint64_t> busy_ns_{0}, bytes_{0}, first_ns_{0}, first_end_ns_{0}, last_ns_{0};
 };

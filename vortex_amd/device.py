@@ -15,7 +15,7 @@ from typing import Optional
 
 import torch
 
-from ._lib import check, lib
+from ._lib import check, lib, tuning
 
 
 def _stream_ptr(stream: Optional[torch.cuda.Stream], device: torch.device) -> int:
@@ -39,7 +39,8 @@ def sha1_uniform(data: torch.Tensor, n: int, piece_len: int, stride: Optional[in
     """Hash n pieces of piece_len bytes at data[i*stride : i*stride+piece_len].
 
     Returns (digests [n,20] or None, matched [n] or None).  Enqueue-only.
-    variant: 0 = default kernel; 1/2 pin a variant (include/vx_tuning.h)."""
+    variant: 0 = the default kernel (vx_sha1_device_uniform, the release
+    library); others pin a variant through the tuning build (vx_tuning.h)."""
     _req(data, "data")
     stride = piece_len if stride is None else stride
     if n and (n - 1) * stride + piece_len > data.numel():
@@ -61,13 +62,15 @@ def sha1_uniform(data: torch.Tensor, n: int, piece_len: int, stride: Optional[in
             _req(matched, "matched")
             if matched.numel() < n or matched.device != dev:
                 raise ValueError("matched must hold n bytes on the data's device")
-    rc = lib().vx_sha1_device_uniform_variant(
-        data.data_ptr(), stride, piece_len, n,
-        digests.data_ptr() if (want_digests and digests is not None) else None,
-        expected.data_ptr() if expected is not None else None,
-        matched.data_ptr() if expected is not None else None,
-        _stream_ptr(stream, dev), variant)
-    check(rc, "vx_sha1_device_uniform")
+    args = (data.data_ptr(), stride, piece_len, n,
+            digests.data_ptr() if (want_digests and digests is not None) else None,
+            expected.data_ptr() if expected is not None else None,
+            matched.data_ptr() if expected is not None else None,
+            _stream_ptr(stream, dev))
+    if variant == 0:
+        check(lib().vx_sha1_device_uniform(*args), "vx_sha1_device_uniform")
+    else:
+        check(tuning().vx_sha1_device_uniform_variant(*args, variant), "vx_sha1_device_uniform_variant", tuning())
     return (digests if want_digests else None), (matched if expected is not None else None)
 
 
@@ -154,10 +157,15 @@ def sha1_ragged(data: torch.Tensor, offsets: torch.Tensor, lens: torch.Tensor,
         rc = lib().vx_sha1_device_ragged_hint(data.data_ptr(), offsets.data_ptr(), lens.data_ptr(), order_p, n,
                                               int(max_len), int(total), digests.data_ptr(), exp_p, m_p,
                                               _stream_ptr(stream, dev))
+        check(rc, "vx_sha1_device_ragged_hint")
+    elif variant == 0:
+        rc = lib().vx_sha1_device_ragged(data.data_ptr(), offsets.data_ptr(), lens.data_ptr(), order_p, n,
+                                         digests.data_ptr(), exp_p, m_p, _stream_ptr(stream, dev))
+        check(rc, "vx_sha1_device_ragged")
     else:
-        rc = lib().vx_sha1_device_ragged_variant(data.data_ptr(), offsets.data_ptr(), lens.data_ptr(), order_p, n,
-                                                 digests.data_ptr(), exp_p, m_p, _stream_ptr(stream, dev), variant)
-    check(rc, "vx_sha1_device_ragged")
+        rc = tuning().vx_sha1_device_ragged_variant(data.data_ptr(), offsets.data_ptr(), lens.data_ptr(), order_p, n,
+                                                    digests.data_ptr(), exp_p, m_p, _stream_ptr(stream, dev), variant)
+        check(rc, "vx_sha1_device_ragged_variant", tuning())
     return digests, matched
 
 
@@ -187,9 +195,10 @@ def length_order(lens_host) -> torch.Tensor:
 def synth_fill(data: torch.Tensor, n: int, piece_len: int, stride: Optional[int] = None, first: int = 0,
                seed: int = 0x5EED0002, corrupt_every: int = 0,
                stream: Optional[torch.cuda.Stream] = None) -> None:
-    """Fill n synthetic pieces on the device (DESIGN.md "Synthetic pieces")."""
+    """Fill n synthetic pieces on the device (DESIGN.md "Synthetic pieces";
+    include/vx_synth.h, a test/bench generator: tuning build only)."""
     _req(data, "data")
     stride = piece_len if stride is None else stride
-    rc = lib().vx_synth_fill(data.data_ptr(), stride, piece_len, n, first, seed, corrupt_every,
-                             _stream_ptr(stream, data.device))
-    check(rc, "vx_synth_fill")
+    rc = tuning().vx_synth_fill(data.data_ptr(), stride, piece_len, n, first, seed, corrupt_every,
+                                _stream_ptr(stream, data.device))
+    check(rc, "vx_synth_fill", tuning())

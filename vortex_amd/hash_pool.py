@@ -74,12 +74,18 @@ class HashPool:
     size, torrent.rs:344).  One HashPool per torrent, used from one thread.
     ``options`` set the other vx_config fields (include/vx_hash.h, ABI 2):
     zero_copy, direct_io, batch_chunk, verify_chunk, verify_cold_chunk,
-    verify_ramp; unset ones keep vx_config_default's values.
+    verify_ramp; unset ones keep vx_config_default's values (each must fit
+    the field's uint32: negative or >= 2**32 values are refused here, ctypes
+    would wrap them silently).  ``hooks=True`` creates the context in the
+    test build libvortex_amd_tuning.so, for fault injection
+    (include/vx_tuning.h); ``self.lib`` is the library holding the context.
     """
 
     def __init__(self, piece_length: int, device: int = 0, slots: Optional[int] = None,
-                 batch_pieces: Optional[int] = None, slot_bytes: Optional[int] = None, **options):
-        L = lib()
+                 batch_pieces: Optional[int] = None, slot_bytes: Optional[int] = None, hooks: bool = False,
+                 **options):
+        L = _lib.tuning() if hooks else lib()
+        self.lib = L
         cfg = vx_config()
         L.vx_config_default(ctypes.byref(cfg), piece_length)
         cfg.device = device
@@ -92,9 +98,11 @@ class HashPool:
         for name, value in options.items():
             if name not in CONFIG_OPTIONS:
                 raise TypeError(f"HashPool: unknown option {name!r} (vx_config has {', '.join(CONFIG_OPTIONS)})")
+            if not 0 <= int(value) < 1 << 32:
+                raise ValueError(f"HashPool: option {name}={value} outside the uint32 range of vx_config")
             setattr(cfg, name, int(value))
         h = ctypes.c_void_p()
-        check(L.vx_create(ctypes.byref(cfg), ctypes.byref(h)), "vx_create")
+        check(L.vx_create(ctypes.byref(cfg), ctypes.byref(h)), "vx_create", L)
         self._h = h
         self.config = cfg
         self._next_tag = 0
@@ -105,7 +113,7 @@ class HashPool:
     # -- lifecycle ---------------------------------------------------------
     def close(self) -> None:
         if self._h:
-            check(lib().vx_destroy(self._h), "vx_destroy")
+            check(self.lib.vx_destroy(self._h), "vx_destroy", self.lib)
             self._h = None
 
     def __enter__(self):
@@ -133,14 +141,14 @@ class HashPool:
         if id(buf) in self._registered:
             raise ValueError("buffer is already registered with this pool")
         addr, keep = _addr_of(buf)
-        check(lib().vx_register_host_buffer(self._h, addr, mv.nbytes), "vx_register_host_buffer")
+        check(self.lib.vx_register_host_buffer(self._h, addr, mv.nbytes), "vx_register_host_buffer", self.lib)
         self._registered[id(buf)] = (addr, keep, buf)
 
     def unregister_buffer(self, buf) -> None:
         ent = self._registered.get(id(buf))
         if ent is None or ent[2] is not buf:
             raise ValueError("buffer was not registered with this pool")
-        check(lib().vx_unregister_host_buffer(self._h, ent[0]), "vx_unregister_host_buffer")
+        check(self.lib.vx_unregister_host_buffer(self._h, ent[0]), "vx_unregister_host_buffer", self.lib)
         del self._registered[id(buf)]
 
     # -- download path -------------------------------------------------------
@@ -163,13 +171,13 @@ class HashPool:
         tag = self._next_tag
         self._next_tag += 1
         if expected_hash is None:
-            rc, where = lib().vx_submit_piece(self._h, tag, addr, piece_len, index), "vx_submit_piece"
+            rc, where = self.lib.vx_submit_piece(self._h, tag, addr, piece_len, index), "vx_submit_piece"
         else:
             exp = ctypes.create_string_buffer(bytes(expected_hash), 20)
-            rc, where = lib().vx_submit(self._h, tag, addr, piece_len, exp), "vx_submit"
+            rc, where = self.lib.vx_submit(self._h, tag, addr, piece_len, exp), "vx_submit"
         if rc != 0:
             try:
-                check(rc, where)
+                check(rc, where, self.lib)
             except VxError as e:
                 e.refused = (index, conn_id, buffer)
                 raise
@@ -181,14 +189,14 @@ class HashPool:
         if len(pieces) % 20:
             raise ValueError("pieces table must be a multiple of 20 bytes")
         buf = ctypes.create_string_buffer(bytes(pieces), max(1, len(pieces)))
-        check(lib().vx_set_piece_table(self._h, buf, len(pieces) // 20), "vx_set_piece_table")
+        check(self.lib.vx_set_piece_table(self._h, buf, len(pieces) // 20), "vx_set_piece_table", self.lib)
 
     def flush(self) -> None:
         """Launch everything queued; call once per event-loop turn."""
-        check(lib().vx_flush(self._h), "vx_flush")
+        check(self.lib.vx_flush(self._h), "vx_flush", self.lib)
 
     def _poll(self, max_items: int) -> list[DownloadedPiece]:
-        k = check(lib().vx_poll(self._h, self._cbuf, min(max_items, len(self._cbuf))), "vx_poll")
+        k = check(self.lib.vx_poll(self._h, self._cbuf, min(max_items, len(self._cbuf))), "vx_poll", self.lib)
         out = []
         for j in range(k):
             r = self._cbuf[j]
@@ -230,32 +238,32 @@ class HashPool:
     def drain(self, timeout_ms: int = 0) -> None:
         """Flush and wait for all in-flight pieces (the scope join of
         event_loop.rs:385-602); results stay queued for try_recv."""
-        check(lib().vx_drain(self._h, timeout_ms), "vx_drain")
+        check(self.lib.vx_drain(self._h, timeout_ms), "vx_drain", self.lib)
 
     @property
     def pending(self) -> int:
-        return int(lib().vx_pending(self._h))
+        return int(self.lib.vx_pending(self._h))
 
     # -- observability (vx_get_stats) -------------------------------------------
     def stats(self) -> dict:
         """The engine's counters (include/vx_hash.h vx_stats) as a dict; the
         latency histogram is a list of VX_STATS_HIST log2 buckets in us."""
         st = vx_stats()
-        check(lib().vx_get_stats(self._h, ctypes.byref(st)), "vx_get_stats")
+        check(self.lib.vx_get_stats(self._h, ctypes.byref(st)), "vx_get_stats", self.lib)
         out = {name: int(getattr(st, name)) for name, _ in vx_stats._fields_ if name != "batch_latency_hist"}
         out["batch_latency_hist"] = [int(x) for x in st.batch_latency_hist]
         return out
 
     def reset_stats(self) -> None:
-        check(lib().vx_reset_stats(self._h), "vx_reset_stats")
+        check(self.lib.vx_reset_stats(self._h), "vx_reset_stats", self.lib)
 
     def last_verify(self) -> dict:
-        """Where the last verify_files call spent its time (vx_tuning.h
-        vx_verify_trace), plus the derived rates bench.py records: the
+        """Where the last verify_files call spent its time (vx_hash.h
+        vx_last_verify), plus the derived rates bench.py records: the
         readers' pread rate, the data copies' GPU-timed rate, and the fraction
         of the copy span the copy engine was busy."""
         t = _lib.vx_verify_trace()
-        check(lib().vx_tuning_last_verify(self._h, ctypes.byref(t)), "vx_tuning_last_verify")
+        check(self.lib.vx_last_verify(self._h, ctypes.byref(t)), "vx_last_verify", self.lib)
         d = {name: getattr(t, name) for name, _ in _lib.vx_verify_trace._fields_}
         gib = float(1 << 30)
         d["read_GiBps_per_thread"] = t.read_bytes / gib / (t.read_busy_ms * 1e-3) if t.read_busy_ms else None
@@ -264,12 +272,23 @@ class HashPool:
         d["copy_busy_frac"] = t.copy_busy_ms / t.copy_span_ms if t.copy_span_ms else None
         return d
 
+    def last_verify_rounds(self) -> list[dict]:
+        """The last verify_files call's round timeline (vx_last_verify_rounds):
+        per chunk round, ms from the call's start — reads queued / done, copy
+        enqueued, the GPU's copy start / end and kernel end — with its bytes,
+        chunk offset, lanes and VX_ROUND_* flags.  Empty on the whole-piece
+        path."""
+        n = check(self.lib.vx_last_verify_rounds(self._h, None, 0), "vx_last_verify_rounds", self.lib)
+        arr = (_lib.vx_verify_round * max(1, n))()
+        n = check(self.lib.vx_last_verify_rounds(self._h, arr, n), "vx_last_verify_rounds", self.lib)
+        return [{name: getattr(arr[k], name) for name, _ in _lib.vx_verify_round._fields_} for k in range(n)]
+
     # -- bulk verify -----------------------------------------------------------
     def sha1_batch(self, pieces: Sequence) -> list[bytes]:
         n = len(pieces)
         ptrs, lens, keep = _ptr_arrays(pieces)
         out = ctypes.create_string_buffer(20 * max(n, 1))
-        check(lib().vx_sha1_batch(self._h, ptrs, lens, n, out), "vx_sha1_batch")
+        check(self.lib.vx_sha1_batch(self._h, ptrs, lens, n, out), "vx_sha1_batch", self.lib)
         raw = out.raw
         return [raw[20 * i: 20 * i + 20] for i in range(n)]
 
@@ -292,7 +311,7 @@ class HashPool:
         exp = ctypes.create_string_buffer(b"".join(bytes(e) for e in expected), 20 * max(n, 1))
         matched = ctypes.create_string_buffer(max(n, 1))
         dig = ctypes.create_string_buffer(20 * max(n, 1))
-        check(lib().vx_verify_batch(self._h, ptrs, lens, exp, n, matched, dig), "vx_verify_batch")
+        check(self.lib.vx_verify_batch(self._h, ptrs, lens, exp, n, matched, dig), "vx_verify_batch", self.lib)
         raw = dig.raw
         return [bool(b) for b in matched.raw[:n]], [raw[20 * i: 20 * i + 20] for i in range(n)]
 
@@ -308,11 +327,11 @@ def _verify_files(pool: "HashPool", paths: Sequence[str], file_lengths: Sequence
     exp = ctypes.create_string_buffer(bytes(expected), max(1, len(expected)))
     out = ctypes.create_string_buffer(max(1, count))
     if first == 0 and count == n:
-        rc = lib().vx_verify_files(pool._h, arr, lens, len(paths), piece_length, exp, n, out, io_threads)
+        rc = pool.lib.vx_verify_files(pool._h, arr, lens, len(paths), piece_length, exp, n, out, io_threads)
     else:
-        rc = lib().vx_verify_files_range(pool._h, arr, lens, len(paths), piece_length, exp, n, first, count, out,
+        rc = pool.lib.vx_verify_files_range(pool._h, arr, lens, len(paths), piece_length, exp, n, first, count, out,
                                          io_threads)
-    bad = check(rc, "vx_verify_files")
+    bad = check(rc, "vx_verify_files", pool.lib)
     return [bool(b) for b in out.raw[:count]], int(bad)
 
 
@@ -324,14 +343,17 @@ def verify_files_multi(pools: Sequence["HashPool"], paths: Sequence[str], file_l
     HashPool.verify_files on one pool: (verdicts, pieces with I/O errors)."""
     if not pools:
         raise ValueError("need at least one pool")
+    L = pools[0].lib
+    if any(p.lib is not L for p in pools):
+        raise ValueError("verify_files_multi: every pool must come from the same library (hooks)")
     n = len(expected) // 20
     ctxs = (ctypes.c_void_p * len(pools))(*[p._h.value for p in pools])
     arr = (ctypes.c_char_p * max(1, len(paths)))(*[os.fsencode(p) for p in paths])
     lens = (ctypes.c_uint64 * max(1, len(file_lengths)))(*file_lengths)
     exp = ctypes.create_string_buffer(bytes(expected), max(1, len(expected)))
     out = ctypes.create_string_buffer(max(1, n))
-    rc = lib().vx_verify_files_multi(ctxs, len(pools), arr, lens, len(paths), piece_length, exp, n, out, io_threads)
-    bad = check(rc, "vx_verify_files_multi")
+    rc = L.vx_verify_files_multi(ctxs, len(pools), arr, lens, len(paths), piece_length, exp, n, out, io_threads)
+    bad = check(rc, "vx_verify_files_multi", L)
     return [bool(b) for b in out.raw[:n]], int(bad)
 
 
@@ -363,7 +385,8 @@ def piece_len(index: int, num_pieces: int, piece_length: int, total_length: int)
     return last if index == num_pieces - 1 else piece_length
 
 
-__all__ = ["DownloadedPiece", "HashPool", "verify_pieces", "verify_files_multi", "piece_len"]
+__all__ = ["DownloadedPiece", "HashPool", "verify_pieces", "verify_files_multi", "piece_len", "plan_verify",
+           "plan_verify_split"]
 
 
 def plan_verify(n_pieces: int, piece_length: int, total_length: int, cpu_threads: int = 0,
@@ -377,4 +400,21 @@ def plan_verify(n_pieces: int, piece_length: int, total_length: int, cpu_threads
                                     ctypes.byref(p)), "vx_plan_verify_gpus")
     out = {name: getattr(p, name) for name, _ in _lib.vx_plan._fields_ if not name.startswith("_")}
     out["use_gpu"] = bool(out["use_gpu"])
+    return out
+
+
+def plan_verify_split(n_pieces: int, piece_length: int, total_length: int, cpu_threads: int = 0,
+                      cpu_thread_rate: float = 0.0, n_gpus: int = 1) -> dict:
+    """Split one bulk verify between the GPUs and the caller's own pool run
+    at once (include/vx_hash.h vx_plan_verify_split, host-only): the GPUs take
+    pieces [gpu_first, n_pieces), the pool the rest; the plan's predicted
+    times for both sides.  gpu_count 0 = keep the pool alone."""
+    p = _lib.vx_plan()
+    first, count = ctypes.c_uint64(), ctypes.c_uint64()
+    check(lib().vx_plan_verify_split(n_pieces, piece_length, total_length, cpu_threads, cpu_thread_rate, n_gpus,
+                                     ctypes.byref(first), ctypes.byref(count), ctypes.byref(p)),
+          "vx_plan_verify_split")
+    out = {name: getattr(p, name) for name, _ in _lib.vx_plan._fields_ if not name.startswith("_")}
+    out["use_gpu"] = bool(out["use_gpu"])
+    out["gpu_first"], out["gpu_count"] = int(first.value), int(count.value)
     return out
