@@ -521,7 +521,7 @@ def copy_gaps(rounds: list, min_ms: float = 0.02) -> dict:
             "first_copy_start_ms": None if first is None else round(first, 3)}
 
 
-def split_call(pool, path: str, total: int, n: int, pl: int, exp: bytes, first: int, io_threads: int,
+def split_call(pool, paths: list, lens: list, n: int, pl: int, exp: bytes, first: int, io_threads: int,
                cpu_threads: int) -> dict:
     """One bulk re-verify split between the GPU and vortex's pool, both at
     once (INTEGRATION.md "Split"): the engine verifies pieces [first, n)
@@ -529,7 +529,9 @@ def split_call(pool, path: str, total: int, n: int, pl: int, exp: bytes, first: 
     re-verify (oracle/pool_oracle.cpp, the par_iter of torrent.rs:724-740;
     the pool's stand-in, kind "port", as in `cpu_pool`) verifies [0, first)
     on cpu_threads threads.  ctypes drops the GIL in both calls, so they run
-    concurrently.  Returns wall time, each side's time and verdict check."""
+    concurrently.  Returns wall time, each side's time, whether every
+    verdict matched, and the merged verdicts (pool's head + engine's tail:
+    the one Box<[bool]> of torrent.rs:727-740)."""
     import threading
 
     import oracle
@@ -539,17 +541,16 @@ def split_call(pool, path: str, total: int, n: int, pl: int, exp: bytes, first: 
     def gpu():
         try:
             t0 = time.perf_counter()
-            got, bad = pool.verify_files([path], [total], pl, exp, io_threads=io_threads, first=first,
-                                         count=n - first)
-            res["gpu"] = (all(got) and bad == 0, time.perf_counter() - t0)
+            got, bad = pool.verify_files(paths, lens, pl, exp, io_threads=io_threads, first=first, count=n - first)
+            res["gpu"] = (all(got) and bad == 0, time.perf_counter() - t0, got)
         except Exception as e:  # noqa: BLE001  (raised below, on the calling thread)
             errs.append(e)
 
     def cpu():
         try:
             t0 = time.perf_counter()
-            ok = oracle.pool_verify_files([path], [total], pl, exp[:20 * first], threads=cpu_threads)
-            res["cpu"] = (all(ok) and len(ok) == first, time.perf_counter() - t0)
+            ok = oracle.pool_verify_files(paths, lens, pl, exp[:20 * first], threads=cpu_threads)
+            res["cpu"] = (all(ok) and len(ok) == first, time.perf_counter() - t0, ok)
         except Exception as e:  # noqa: BLE001
             errs.append(e)
 
@@ -563,7 +564,9 @@ def split_call(pool, path: str, total: int, n: int, pl: int, exp: bytes, first: 
     if errs:
         raise errs[0]
     ok = all(v[0] for v in res.values())
-    return {"s": wall, "gpu_s": res.get("gpu", (True, 0.0))[1], "cpu_s": res.get("cpu", (True, 0.0))[1], "ok": ok}
+    merged = list(res.get("cpu", (0, 0, []))[2]) + list(res.get("gpu", (0, 0, []))[2])
+    return {"s": wall, "gpu_s": res.get("gpu", (True, 0.0))[1], "cpu_s": res.get("cpu", (True, 0.0))[1], "ok": ok,
+            "matched": merged}
 
 
 def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 5):
@@ -641,15 +644,20 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 5):
             plan = plan_verify_split(n, pl, total, cpu_threads=threads, cpu_thread_rate=total / cw / threads)
             split = {"plan": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in plan.items()},
                      "configs": []}
-            for io_t, cpu_th in ((threads, threads), (max(2, threads // 2), threads)):
-                calls = [split_call(pool, path, total, n, pl, exp, plan["gpu_first"], io_t, cpu_th)
-                         for _ in range(split_reps)]
-                assert all(c["ok"] for c in calls), "split re-verify: a verdict differs from the expected table"
-                med = sorted(calls, key=lambda c: c["s"])[len(calls) // 2]
-                split["configs"].append({"io_threads": io_t, "cpu_threads": cpu_th,
-                                         "value": round(total / med["s"] / GiB, 2),
-                                         "s_runs": [round(c["s"], 4) for c in calls],
-                                         "gpu_s": round(med["gpu_s"], 4), "cpu_s": round(med["cpu_s"], 4)})
+            # the planner's split point and two with less on the GPU side, with the engine's
+            # readers at half and a quarter of the pool's threads (they share the host's cores)
+            k0 = plan["gpu_count"]
+            points = sorted({n - k0, n - int(k0 * 0.9), n - int(k0 * 0.8)}) if k0 else [n]
+            for io_t in (max(2, threads // 2), max(2, threads // 4)):
+                for first in points:
+                    calls = [split_call(pool, [path], [total], n, pl, exp, first, io_t, threads)
+                             for _ in range(split_reps)]
+                    assert all(c["ok"] for c in calls), "split re-verify: a verdict differs from the expected table"
+                    med = sorted(calls, key=lambda c: c["s"])[len(calls) // 2]
+                    split["configs"].append({"io_threads": io_t, "cpu_threads": threads, "gpu_first": first,
+                                             "planned": first == n - k0, "value": round(total / med["s"] / GiB, 2),
+                                             "s_runs": [round(c["s"], 4) for c in calls],
+                                             "gpu_s": round(med["gpu_s"], 4), "cpu_s": round(med["cpu_s"], 4)})
     finally:
         if os.path.exists(path):
             os.unlink(path)
@@ -680,14 +688,19 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 5):
 
     warm, cold = record("warm"), record("cold")
     best = max(split["configs"], key=lambda c: c["value"])
-    split.update({"value": best["value"], "unit": "GiB/s", "gpu_only": warm["value"],
+    planned = [c for c in split["configs"] if c["planned"]]
+    split.update({"value": best["value"], "unit": "GiB/s", "best_gpu_first": best["gpu_first"],
+                  "best_io_threads": best["io_threads"],
+                  "planned_value": max(c["value"] for c in planned) if planned else None,
+                  "gpu_only": warm["value"],
                   "pool_only": warm["cpu_pool"]["value"],
                   "beats_both": best["value"] > max(warm["value"], warm["cpu_pool"]["value"]),
                   "pool_kind": "port",
-                  "sample": f"the warm file split by vx_plan_verify_split: GPU pieces [{split['plan']['gpu_first']}, {n}) "
-                            f"via vx_verify_files_range while the CPU pool restatement (vortex's par_iter stand-in) "
-                            f"verifies [0, {split['plan']['gpu_first']}) at once; median of {split_reps} per "
-                            f"(engine readers, pool threads) config; every verdict checked"})
+                  "sample": f"the warm file split at GPU pieces [first, {n}) via vx_verify_files_range while the CPU "
+                            f"pool restatement (vortex's par_iter stand-in, {threads} threads) verifies [0, first) at "
+                            f"once; first = vx_plan_verify_split's {split['plan']['gpu_first']} and two points with "
+                            f"10 / 20 % fewer GPU pieces, engine readers at 1/2 and 1/4 of the pool's threads; "
+                            f"median of {split_reps} per config; every verdict checked"})
     warm["split"] = split
     where = {"dir": d, "fs": fs_type(d)}
     warm.update({"write_s": round(t_write, 2), "file": where,

@@ -68,6 +68,32 @@ def test_verify_files_range(built, gpu, tmp_path, pl):
             assert e.value.code == VX_EINVAL
 
 
+@pytest.mark.parametrize("pl", [256 * 1024, 1 << 20])
+def test_split_verify_with_the_pool(built, gpu, tmp_path, pl):
+    """The split re-verify (INTEGRATION.md "The split", bench.py reverify.split):
+    the engine verifies the tail [first, n) with vx_verify_files_range while
+    the CPU pool restatement (vortex's par_iter stand-in) verifies the head
+    [0, first), both at once on one damaged multi-file torrent; the merged
+    verdicts equal the pool's over the whole torrent at every split point,
+    and vx_plan_verify_split's point lies in range."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from vortex_amd.hash_pool import HashPool, plan_verify_split
+
+    sizes = [3, 4 * pl + 17, 2 * pl, 0, 3 * pl - 5, pl + 1, 64, 2 * pl + pl // 2]
+    paths, exp = _torrent(tmp_path, pl, sizes, 23)
+    n = len(exp) // 20
+    _damage(paths, pl)
+    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
+    plan = plan_verify_split(n, pl, sum(sizes), cpu_threads=4)
+    assert plan["gpu_first"] + plan["gpu_count"] == n
+    with HashPool(pl, slots=3, batch_pieces=4, slot_bytes=3 << 20) as pool:
+        for first in sorted({0, 1, n // 2, n - 1, n, plan["gpu_first"]}):
+            r = bench.split_call(pool, paths, sizes, n, pl, exp, first, 3, 4)
+            assert r["matched"] == want, first
+            assert r["ok"] is False  # the damaged pieces mismatch on whichever side holds them
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

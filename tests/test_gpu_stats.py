@@ -11,10 +11,12 @@ the latency histogram must account for every harvested batch.
 import hashlib
 import mmap
 import random
+import sys
 
 import pytest
 
 import oracle
+from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
 
@@ -157,7 +159,7 @@ def test_stats_reverify(built, gpu, tmp_path, pl):
         assert st["pieces_mismatched"] == 1  # I/O errors are counted once, in io_errors
         assert (st["chunk_rounds"] > 0) == (pl >= 1 << 20)
         _check_latency(st)
-        # the call's time budget (vx_tuning_last_verify, recorded per call by bench.py)
+        # the call's time budget (vx_last_verify, recorded per call by bench.py)
         tr = pool.last_verify()
         assert tr["read_bytes"] == len(whole)  # every piece byte requested once (failed reads included)
         assert 0 < tr["read_busy_ms"] and 0 < tr["first_read_ms"] <= tr["wall_ms"] and tr["read_span_ms"] <= tr["wall_ms"]
@@ -167,3 +169,28 @@ def test_stats_reverify(built, gpu, tmp_path, pl):
             assert 0 < tr["copy_busy_ms"] <= tr["copy_span_ms"] + 1e-3 and 0 < tr["copy_busy_frac"] <= 1.0001
         else:
             assert tr["rounds"] == 0 and tr["copy_bytes"] == 0
+        # the round timeline (vx_last_verify_rounds): one record per timed round, times on the
+        # call's clock in order: reads queued <= done <= enqueued; copy start <= end <= kernel end
+        rounds = pool.last_verify_rounds()
+        if pl < 1 << 20:
+            assert rounds == []
+        else:
+            from vortex_amd._lib import VX_ROUND_HEAD_RAMP, VX_ROUND_NEW_WINDOW, VX_ROUND_TAIL_RAMP
+
+            assert len(rounds) == tr["rounds"] and sum(r["bytes"] for r in rounds) == tr["copy_bytes"]
+            assert rounds[0]["flags"] & VX_ROUND_NEW_WINDOW and rounds[0]["offset"] == 0
+            assert any(r["flags"] & VX_ROUND_HEAD_RAMP for r in rounds) and rounds[-1]["flags"] & VX_ROUND_TAIL_RAMP
+            slack = 0.5  # ms: the GPU-to-host clock mapping's error (the anchor event's dispatch latency)
+            for a, b in zip(rounds, rounds[1:]):
+                assert b["copy_start_ms"] >= a["copy_end_ms"] - 1e-3  # copies are chained across slots
+                assert b["enqueue_ms"] >= a["enqueue_ms"]
+            for r in rounds:
+                assert 0 <= r["read_submit_ms"] <= r["read_done_ms"] <= r["enqueue_ms"] <= tr["wall_ms"]
+                assert r["enqueue_ms"] - slack <= r["copy_start_ms"] <= r["copy_end_ms"] <= r["kernel_end_ms"]
+                assert r["kernel_end_ms"] <= tr["wall_ms"] + slack and r["lanes"] >= 1
+            sys.path.insert(0, ROOT)
+            import bench
+
+            gaps = bench.copy_gaps(rounds)
+            assert gaps["rounds"] == len(rounds) and gaps["gap_ms"] >= 0
+            assert set(gaps["by_cause"]) <= {"read", "hand-off", "device"}

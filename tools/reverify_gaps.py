@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Where the warm config-5 re-verify's copy engine idles:
+vx_verify_files over the linux-mint-geometry file for several context shapes,
+alternating, each call's round timeline (vx_last_verify_rounds) reduced by
+bench.copy_gaps to gaps by cause and by slot.  Prints one JSON line.
+
+Shapes: "<slots>" (the engine's default: copies on the context's copy
+stream) or "<slots>s" (each copy on its slot's stream, round 4's form:
+vx_tuning_verify_copy_stream(ctx, 0), test build).
+
+usage: python tools/reverify_gaps.py [--reps 5] [--slots 4,4s,6,6s] [--scale 1.0]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--slots", default="4,4s,6,6s")
+    ap.add_argument("--scale", type=float, default=1.0)
+    a = ap.parse_args()
+    import bench
+    import oracle
+    from vortex_amd.hash_pool import HashPool
+
+    pl = 2097152
+    threads = bench.cpu_share()
+    path = os.path.join(bench.reverify_dir(), f"vx_gaps_{os.getpid()}.iso")
+    out = {"threads": threads, "shapes": {}}
+    try:
+        total, n, last = bench.write_linuxmint_file(path, a.scale)
+        exp = oracle.pool_digest_synth(0x5EED0005, 0, n, pl, last_index=n - 1, last_len=last, threads=threads)
+        shapes = a.slots.split(",")
+        pools = {}
+        for s in shapes:
+            pools[s] = HashPool(pl, slots=int(s.rstrip("s")), slot_bytes=512 << 20, batch_pieces=4096, hooks=True)
+            pools[s].lib.vx_tuning_verify_copy_stream(pools[s]._h, 0 if s.endswith("s") else 1)
+        runs = {s: [] for s in shapes}
+        for s, pool in pools.items():  # warm every context (stages, rows, page cache)
+            got, bad = pool.verify_files([path], [total], pl, exp, io_threads=threads)
+            assert all(got) and bad == 0
+        for _ in range(a.reps):
+            for s, pool in pools.items():
+                t0 = time.perf_counter()
+                got, bad = pool.verify_files([path], [total], pl, exp, io_threads=threads)
+                el = time.perf_counter() - t0
+                assert all(got) and bad == 0
+                rounds = pool.last_verify_rounds()
+                tr = pool.last_verify()
+                g = bench.copy_gaps(rounds)
+                by_slot = {}
+                ns = int(s.rstrip("s"))
+                for k in range(1, len(rounds)):
+                    gap = rounds[k]["copy_start_ms"] - rounds[k - 1]["copy_end_ms"]
+                    by_slot[k % ns] = round(by_slot.get(k % ns, 0.0) + max(0.0, gap), 3)
+                # copies that started within 0.1 ms of the previous round's kernel end
+                after_kernel = sum(1 for k in range(1, len(rounds))
+                                   if 0 <= rounds[k]["copy_start_ms"] - rounds[k - 1]["kernel_end_ms"] < 0.1)
+                runs[s].append({"GiBps": round(total / el / (1 << 30), 2), "copy_busy_frac": round(tr["copy_busy_frac"], 3),
+                                "gap_ms": g["gap_ms"], "by_cause": g["by_cause"], "gap_ms_by_slot": by_slot,
+                                "copy_after_prev_kernel": after_kernel})
+        for s in shapes:
+            r = sorted(runs[s], key=lambda x: x["GiBps"])
+            out["shapes"][f"slots{s}"] = {"median_GiBps": r[len(r) // 2]["GiBps"], "runs": runs[s]}
+        for p in pools.values():
+            p.close()
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()

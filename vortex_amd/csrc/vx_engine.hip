@@ -208,6 +208,13 @@ struct vx_ctx {
     vx_verify_trace last_verify{};
     std::vector<hipEvent_t> copy_ev;
     std::vector<vx_verify_round> last_rounds;  // vx_last_verify_rounds
+    // The file re-verify's chunk rounds put every H2D on this one stream (high
+    // priority: its own hardware queue) and only kernels on the slot streams,
+    // so no copy ever sits behind a kernel.  Created on first
+    // use.  verify_copy_stream = 0 (test build only) restores the slot-stream
+    // copies for A/B.
+    hipStream_t copy_stream = nullptr;
+    int verify_copy_stream = 1;
     hipEvent_t anchor_ev = nullptr;            // maps the rounds' GPU times onto the host clock
     uint64_t verify_t0_ns = 0;                 // the running re-verify call's start (steady clock)
 };
@@ -850,6 +857,10 @@ int vx_destroy(vx_ctx* c) {
     for (hipEvent_t e : c->copy_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->anchor_ev) (void)hipEventDestroy(c->anchor_ev);
+    if (c->copy_stream) {
+        (void)hipStreamSynchronize(c->copy_stream);
+        (void)hipStreamDestroy(c->copy_stream);
+    }
     delete c;
     return rc;
 }
@@ -1161,8 +1172,28 @@ struct ChunkPipe {
     uint8_t *d_exp = nullptr, *d_dig = nullptr, *d_match = nullptr;
     hipEvent_t prev_kernel = nullptr;
     bool have_prev = false;
+    // Set (use_copy_stream): every round's H2D goes on the context's copy
+    // stream, its kernel on the slot's stream after a wait on the round's
+    // `copied` event.  Two slot streams can share one hardware queue (HIP maps
+    // streams onto GPU_MAX_HW_QUEUES = 4), and a copy queued behind the other
+    // slot's kernel there waited for that kernel: 5-7 ms of idle PCIe per
+    // warm linux-mint call with 4-6 slots (profiles/r05/gaps/).
+    hipStream_t cs = nullptr;
 
     explicit ChunkPipe(vx_ctx* ctx) : c(ctx) {}
+
+    int use_copy_stream() {
+        if (!c->copy_stream) {
+            int least = 0, greatest = 0;
+            if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+                hipStreamCreateWithPriority(&c->copy_stream, hipStreamNonBlocking, greatest) != hipSuccess) {
+                c->copy_stream = nullptr;
+                return fail(VX_EDEVICE, "chunk rounds: copy stream creation failed");
+            }
+        }
+        cs = c->copy_stream;
+        return 0;
+    }
     ~ChunkPipe() { release(); }
     ChunkPipe(const ChunkPipe&) = delete;
     ChunkPipe& operator=(const ChunkPipe&) = delete;
@@ -1236,6 +1267,7 @@ struct ChunkPipe {
     // continues = the round follows one of the same window.
     template <class F>
     int round(int si, uint32_t m, bool continues, bool meta_first, F&& copy_data) {
+        if (cs) return round_cs(si, m, continues, copy_data);
         Slot& s = c->slots[si];
         hipStream_t st = s.stream;
         int rc = chain_h2d(c, si);
@@ -1264,6 +1296,40 @@ struct ChunkPipe {
         s.state = Slot::INFLIGHT;
         s.seq = c->seq++;
         s.n = 0;  // nothing to harvest: outputs live in the call's device rows
+        if (!rc) rc = reap(c, false);
+        return rc;
+    }
+    // round() with the copies on the copy stream: data, then the lane table,
+    // then `copied`; the slot's stream waits for it and runs the kernel.  The
+    // copies stay in launch order (one stream), with no host wait between
+    // them; the slot is reused only after its `done` (free_slot), so no copy
+    // overwrites a stage or arena a kernel still reads.
+    template <class F>
+    int round_cs(int si, uint32_t m, bool continues, F&& copy_data) {
+        Slot& s = c->slots[si];
+        hipStream_t st = s.stream;
+        const size_t meta = (size_t)(reinterpret_cast<const uint8_t*>(s.h_pidx + m) - reinterpret_cast<const uint8_t*>(s.h_offsets));
+        int rc = copy_data(s, cs);
+        if (!rc && hipMemcpyAsync(s.d_offsets, s.h_offsets, meta, hipMemcpyHostToDevice, cs) != hipSuccess)
+            rc = fail(VX_EDEVICE, "chunk round: H2D failed");
+        if (!rc && hipEventRecord(s.copied, cs) != hipSuccess) rc = fail(VX_EDEVICE, "chunk round: event failed");
+        mark_launched(c, si);
+        if (!rc && hipStreamWaitEvent(st, s.copied, 0) != hipSuccess)
+            rc = fail(VX_EDEVICE, "chunk round: stream wait failed");
+        if (!rc && continues && have_prev && hipStreamWaitEvent(st, prev_kernel, 0) != hipSuccess)
+            rc = fail(VX_EDEVICE, "chunk round: stream wait failed");
+        if (!rc) {
+            hipError_t e = vx::launch_chunk(s.d_arena, s.d_offsets, s.d_lens, m, s.d_pidx, s.d_poff, s.d_tlen,
+                                            d_states, d_dig, d_exp, d_match, st);
+            if (e != hipSuccess) rc = hip_fail(e, "chunk kernel launch");
+        }
+        if (!rc && (hipEventRecord(prev_kernel, st) != hipSuccess || hipEventRecord(s.done, st) != hipSuccess))
+            rc = fail(VX_EDEVICE, "chunk round: event record failed");
+        have_prev = true;
+        c->stats.chunk_rounds++;
+        s.state = Slot::INFLIGHT;
+        s.seq = c->seq++;
+        s.n = 0;
         if (!rc) rc = reap(c, false);
         return rc;
     }
@@ -1354,6 +1420,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     const uint64_t cnt = end - first;
     ChunkPipe cp(c);
     int rc = cp.open(cnt, fv.expected + 20 * first, "vx_verify_files");
+    if (!rc && c->verify_copy_stream) rc = cp.use_copy_stream();
     cp.bytes = cnt * (uint64_t)pl - (end == n ? (uint64_t)pl - last_len : 0);
     // windows of W pieces; each window runs its rounds in order
     const Slot& s0 = c->slots[0];
@@ -2161,6 +2228,9 @@ void vx_tuning_fail_submit_after(vx_ctx* c, int64_t k) {
 }
 void vx_tuning_fail_launch_after(vx_ctx* c, int64_t k) {
     if (c) c->fail_launch_after = k < 0 ? -1 : k;
+}
+void vx_tuning_verify_copy_stream(vx_ctx* c, int on) {
+    if (c) c->verify_copy_stream = on ? 1 : 0;
 }
 #endif
 size_t vx_tuning_chunk_schedule(uint64_t L, uint64_t C, int head, int tail, uint64_t* out, size_t max) {
