@@ -2103,15 +2103,19 @@ namespace {
 constexpr double kChainBlock = 0.76e-6, kPcieRate = 52.0 * (1ull << 30), kSetup = 1.5e-3;
 constexpr double kOverlapLoss = 0.08, kMargin = 1.1;
 constexpr double kBatchLatency = 1e-3;  // launch, H2D of a small batch, D2H, poll
-// One reader thread's pread rate from the page cache (a memcpy out of the
-// cache; 7.4-7.8 GiB/s measured per reader, BENCH_r04 reverify.gpu_traces):
-// the host CPU time the GPU side of a split takes from the caller's pool.
-constexpr double kReadRate = 8.0e9;
+// A split runs the GPU side's reads beside the pool's hashing on the same
+// host: each reader byte costs the pool rate / kReadRate of a hashed byte, and
+// the GPU side's bytes move at kSplitLink of the link rate (page-cache reads,
+// stage writes and DMA share host memory with the pool).  Fitted to the warm
+// config-5 split on one box (profiles/r05/split/: GPU side 41 GB/s, pool 0.83
+// of its rate alone, best split 770 of 1,387 pieces to the GPU).
+constexpr double kReadRate = 16.0e9, kSplitLink = 0.74;
 
-// The GPU path over `bytes` bytes of pieces piece_length long, over n_gpus links.
-void plan_gpu(double L, double bytes, uint32_t n_gpus, vx_plan* out) {
+// The GPU path over `bytes` bytes of pieces piece_length long, over n_gpus links
+// at `link` of the PCIe rate.
+void plan_gpu(double L, double bytes, uint32_t n_gpus, vx_plan* out, double link = 1.0) {
     out->gpu_chain_s = std::ceil((L + 9) / 64) * kChainBlock;
-    out->gpu_transfer_s = bytes / kPcieRate / std::max<uint32_t>(1, n_gpus);
+    out->gpu_transfer_s = bytes / (kPcieRate * link) / std::max<uint32_t>(1, n_gpus);
     out->gpu_s = std::max(out->gpu_transfer_s, out->gpu_chain_s) + kSetup +
                  kOverlapLoss * std::min(out->gpu_transfer_s, out->gpu_chain_s);
 }
@@ -2162,7 +2166,7 @@ int vx_plan_verify_split(uint64_t n_pieces, uint32_t piece_length, uint64_t tota
     double best_t = cpu_time(0);
     const double pool_alone = best_t;
     for (uint64_t k = 1; k <= n_pieces; ++k) {
-        plan_gpu(L, gpu_bytes(k), n_gpus, &g);
+        plan_gpu(L, gpu_bytes(k), n_gpus, &g, k < n_pieces ? kSplitLink : 1.0);
         const double t = std::max(g.gpu_s, cpu_time(k));
         if (t < best_t) best_t = t, best_k = k;
     }
@@ -2171,7 +2175,7 @@ int vx_plan_verify_split(uint64_t n_pieces, uint32_t piece_length, uint64_t tota
     *gpu_first = n_pieces - best_k;
     if (out) {
         *out = vx_plan{};
-        if (best_k) plan_gpu(L, gpu_bytes(best_k), n_gpus, out);
+        if (best_k) plan_gpu(L, gpu_bytes(best_k), n_gpus, out, best_k < n_pieces ? kSplitLink : 1.0);
         out->cpu_s = cpu_time(best_k);
         vx_plan one{};
         plan_gpu(L, L, 1, &one);  // the download path's figures do not depend on the split
