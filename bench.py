@@ -569,7 +569,7 @@ def split_call(pool, paths: list, lens: list, n: int, pl: int, exp: bytes, first
             "matched": merged}
 
 
-def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 5):
+def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
     """BASELINE config 5: full re-verify of a torrent's data from disk with
     the linux-mint geometry (cli/linux-mint.torrent: 2,907,832,320 B, 2 MiB
     pieces, last 1,179,648 B) through vx_verify_files (pread into pinned
@@ -640,25 +640,36 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 5):
             for _ in range(2):
                 resident_fraction(path)  # cached again after the cold leg: read it once through
                 oracle.pool_verify_files([path], [total], pl, exp, threads=threads)
+            # The pool beside the engine gets 3/4 of the threads, the engine 8 readers (half):
+            # a full-size pool beside them oversubscribed the host and ran bimodal, 38-71 ms a
+            # call; 12 + 8 ran 48 +- 0.5 ms (profiles/r05/split/sweep.json)
             cw = sorted(legs["warm"][1])[len(legs["warm"][1]) // 2]
-            plan = plan_verify_split(n, pl, total, cpu_threads=threads, cpu_thread_rate=total / cw / threads)
+            rate = total / cw / threads
+            pool_t, io_t = max(1, threads * 3 // 4), max(2, threads // 2)
+            plan = plan_verify_split(n, pl, total, cpu_threads=pool_t, cpu_thread_rate=rate)
             split = {"plan": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in plan.items()},
                      "configs": []}
-            # the planner's split point and one either side (10 % more / fewer GPU pieces), the
-            # engine's readers at half the pool's threads (they share the host's cores; 1/4 and
-            # all of them measured slower, profiles/r05/split/)
+            # the planner's split point and one either side (10 % more / fewer GPU pieces)
             k0 = plan["gpu_count"]
             points = sorted({n - k0, n - int(k0 * 0.9), max(0, n - int(k0 * 1.1))}) if k0 else [n]
-            for io_t in (max(2, threads // 2),):
-                for first in points:
-                    calls = [split_call(pool, [path], [total], n, pl, exp, first, io_t, threads)
-                             for _ in range(split_reps)]
-                    assert all(c["ok"] for c in calls), "split re-verify: a verdict differs from the expected table"
-                    med = sorted(calls, key=lambda c: c["s"])[len(calls) // 2]
-                    split["configs"].append({"io_threads": io_t, "cpu_threads": threads, "gpu_first": first,
-                                             "planned": first == n - k0, "value": round(total / med["s"] / GiB, 2),
-                                             "s_runs": [round(c["s"], 4) for c in calls],
-                                             "gpu_s": round(med["gpu_s"], 4), "cpu_s": round(med["cpu_s"], 4)})
+            # The points alternate call by call with the GPU alone (all readers) and the pool
+            # alone (all threads) as references, so a box's drift lands on all of them alike.
+            cfgs = [(first, io_t, pool_t) for first in points] + [(0, threads, threads), (n, threads, threads)]
+            by_cfg = {c: [] for c in cfgs}
+            for _ in range(split_reps):
+                for c in cfgs:
+                    by_cfg[c].append(split_call(pool, [path], [total], n, pl, exp, c[0], c[1], c[2]))
+            for (first, io_c, pool_c), calls in by_cfg.items():
+                assert all(c["ok"] for c in calls), "split re-verify: a verdict differs from the expected table"
+                med = sorted(calls, key=lambda c: c["s"])[len(calls) // 2]
+                entry = {"io_threads": io_c, "cpu_threads": pool_c, "gpu_first": first,
+                         "planned": first == n - k0 and io_c == io_t, "value": round(total / med["s"] / GiB, 2),
+                         "s_runs": [round(c["s"], 4) for c in calls],
+                         "gpu_s": round(med["gpu_s"], 4), "cpu_s": round(med["cpu_s"], 4)}
+                if first in (0, n) and io_c == threads:
+                    split["gpu_alone" if first == 0 else "pool_alone"] = entry
+                else:
+                    split["configs"].append(entry)
     finally:
         if os.path.exists(path):
             os.unlink(path)
@@ -693,15 +704,15 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 5):
     split.update({"value": best["value"], "unit": "GiB/s", "best_gpu_first": best["gpu_first"],
                   "best_io_threads": best["io_threads"],
                   "planned_value": max(c["value"] for c in planned) if planned else None,
-                  "gpu_only": warm["value"],
-                  "pool_only": warm["cpu_pool"]["value"],
-                  "beats_both": best["value"] > max(warm["value"], warm["cpu_pool"]["value"]),
+                  "gpu_only": split["gpu_alone"]["value"], "pool_only": split["pool_alone"]["value"],
+                  "beats_both": best["value"] > max(split["gpu_alone"]["value"], split["pool_alone"]["value"]),
                   "pool_kind": "port",
                   "sample": f"the warm file split at GPU pieces [first, {n}) via vx_verify_files_range while the CPU "
-                            f"pool restatement (vortex's par_iter stand-in, {threads} threads) verifies [0, first) at "
-                            f"once; first = vx_plan_verify_split's {split['plan']['gpu_first']} and the points with "
-                            f"10 % fewer / more GPU pieces, engine readers at half the pool's threads; "
-                            f"median of {split_reps} per config; every verdict checked"})
+                            f"pool restatement (vortex's par_iter stand-in, 3/4 of the {threads} threads) verifies "
+                            f"[0, first) at once; first = vx_plan_verify_split's {split['plan']['gpu_first']} and the "
+                            f"points with 10 % fewer / more GPU pieces, engine readers at half the threads; "
+                            f"alternating call by call with the GPU alone and the pool alone (gpu_only / "
+                            f"pool_only); median of {split_reps} per config; every verdict checked"})
     warm["split"] = split
     where = {"dir": d, "fs": fs_type(d)}
     warm.update({"write_s": round(t_write, 2), "file": where,
@@ -794,6 +805,7 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
     cpu = {"warm": [], "cold": []}
     cpu_ok = True
     pool = None
+    split = None
     try:
         try:
             pool = HashPool(pl, device=local, slots=4, slot_bytes=512 << 20, batch_pieces=4096)
@@ -848,6 +860,7 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
                         log(f"CPU pool re-verify failed: {type(e).__name__}: {e}")
                         cpu_ok = False
                 dist.barrier()
+        split = multi_split(rank, world, pool, path, total, n, exp, io_threads, ncpu, cpu, agree, reps)
     finally:
         if pool is not None:
             pool.close()
@@ -879,6 +892,12 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
                    "use_gpu": p["use_gpu"], "predicted_GiBps": round(total / p["gpu_s"] / GiB, 2),
                    "model": "vx_plan_verify_gpus (DESIGN.md §6.6), n_gpus = ranks, the CPU pool's measured warm "
                             "rate per thread"}
+    if split is not None:
+        split["value"] = round(total / split["s"] / GiB, 2)
+        split.update({"unit": "GiB/s", "gpu_only": out["warm"]["value"],
+                      "pool_only": out["warm"]["cpu_pool"]["value"] if out["warm"]["cpu_pool"] else None})
+        split["beats_both"] = split["value"] > max(v for v in (split["gpu_only"], split["pool_only"]) if v)
+        out["split"] = split
     out.update({"ranks": world, "same_device": same_device, "io_threads_per_rank": io_threads,
                 "pieces": n, "bytes": total, "write_s": round(spec["write_s"], 2), "cpu_pool_verdicts_ok": cpu_ok,
                 "file": {"dir": spec["dir"], "fs": fs_type(spec["dir"])},
@@ -887,6 +906,86 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
                           f"warm median of {reps}, cold (evicted) median of {cold_reps}; the slowest rank's time; "
                           f"CPU pool restatement with all {ncpu} node CPUs beside it"})
     return out
+
+
+def multi_split(rank, world, pool, path, total, n, exp, io_threads, ncpu, cpu, agree, reps):
+    """The split over a node (INTEGRATION.md "The split"): rank
+    0 plans with vx_plan_verify_split (n_gpus = ranks, the pool on 3/4 of the
+    node's CPUs at the warm rate it just measured); every rank verifies its
+    share of the GPU tail [first, n) on its GPU while rank 0's CPU pool
+    restatement verifies the head [0, first) beside it.  A call's time is the
+    slowest of all; every verdict is gathered and checked.  Warm only.
+    Returns the record on rank 0 (None elsewhere)."""
+    import threading
+
+    import torch
+    import torch.distributed as dist
+
+    import oracle
+    from vortex_amd import shard
+    from vortex_amd.hash_pool import plan_verify_split
+
+    pl = 2097152
+    obj = [None]
+    if rank == 0:
+        cw = sorted(cpu["warm"])[len(cpu["warm"]) // 2] if cpu["warm"] else None
+        rate = total / cw / ncpu if cw else 0.0
+        obj = [plan_verify_split(n, pl, total, cpu_threads=max(1, ncpu * 3 // 4), cpu_thread_rate=rate,
+                                 n_gpus=world)]
+    dist.broadcast_object_list(obj, src=0)
+    plan = obj[0]
+    first = plan["gpu_first"]
+    sub_first, sub_count = shard.shard_range(n - first, world, rank)
+    times, head_ok, tail_ok = [], True, True
+    for _ in range(reps):
+        dist.barrier()
+        res = {}
+
+        def head():
+            t0 = time.perf_counter()
+            res["head"] = oracle.pool_verify_files([path], [total], pl, exp[:20 * first],
+                                                   threads=max(1, ncpu * 3 // 4))
+            res["head_s"] = time.perf_counter() - t0
+
+        th = threading.Thread(target=head) if rank == 0 and first else None
+        ok = True
+        try:
+            t0 = time.perf_counter()
+            if th:
+                th.start()
+            got, bad = (pool.verify_files([path], [total], pl, exp, io_threads=io_threads, first=first + sub_first,
+                                          count=sub_count) if sub_count else ([], 0))
+            gpu_s = time.perf_counter() - t0
+            if th:
+                th.join()
+            el = time.perf_counter() - t0
+        except Exception as e:  # noqa: BLE001
+            log(f"rank {rank}: split call failed: {type(e).__name__}: {e}")
+            ok = False
+        if not agree(ok):
+            raise RuntimeError("multi-GPU split re-verify: a rank's call failed")
+        vdev = torch.device("cpu") if dist.get_backend() == "gloo" else torch.device("cuda", torch.cuda.current_device())
+        tail = shard.gather_verdicts(torch.tensor(got, dtype=torch.uint8, device=vdev), n - first) if n - first else None
+        allt = [None] * world
+        dist.all_gather_object(allt, {"s": el, "gpu_s": gpu_s, "bad": bad})
+        tail_ok = tail_ok and (tail is None or int(tail.sum()) == n - first) and not any(t["bad"] for t in allt)
+        if rank == 0:
+            head_ok = head_ok and (not first or (len(res["head"]) == first and all(res["head"])))
+            times.append({"s": max(t["s"] for t in allt), "gpu_s": max(t["gpu_s"] for t in allt),
+                          "cpu_s": res.get("head_s", 0.0)})
+    if not tail_ok:  # the same on every rank
+        raise RuntimeError("multi-GPU split re-verify: verdicts differ from the expected table")
+    if rank != 0:
+        return None
+    if not head_ok:
+        raise RuntimeError("multi-GPU split re-verify: the pool's head verdicts differ from the expected table")
+    med = sorted(times, key=lambda t: t["s"])[len(times) // 2]
+    return {"s": med["s"], "gpu_s": round(med["gpu_s"], 4), "cpu_s": round(med["cpu_s"], 4),
+            "s_runs": [round(t["s"], 4) for t in times], "gpu_first": first, "gpu_count": n - first,
+            "pool_threads": max(1, ncpu * 3 // 4),
+            "plan": {k: (round(v, 5) if isinstance(v, float) else v) for k, v in plan.items()},
+            "sample": "warm; GPU ranks verify [gpu_first, n) split by index while rank 0's CPU pool restatement "
+                      "verifies [0, gpu_first) at once; the slowest side's time, median; every verdict checked"}
 
 
 def roofline(n: int, plen: int, kern_ms: float, achieved: float, workload: str, clock: dict | None = None,

@@ -350,12 +350,14 @@ int vx_plan_verify_gpus(uint64_t n_pieces, uint32_t piece_length, uint64_t total
  * running at once (torrent.rs:724-740's par_iter over the pool's range, and
  * vx_verify_files_range / _multi over the GPUs' range): the GPUs take the
  * contiguous tail [*gpu_first, n_pieces), *gpu_count pieces, chosen so the
- * predicted GPU time (the same model, over n_gpus) equals the pool's time on
- * the rest; the last piece (the short one) goes to whichever side holds the
- * tail.  *gpu_count is 0 when the pool alone is faster than any split, and
- * n_pieces when the GPUs alone are.  out (may be NULL) gets the plan of the
- * split: gpu_s for the GPUs' range, cpu_s for the pool's, use_gpu = 1 when
- * the split beats both sides alone by the 10 % margin. */
+ * predicted GPU time (the same model over n_gpus, its bytes at 0.74 of the
+ * link: the pool shares host memory) meets the pool's time on the rest.
+ * cpu_threads is the pool that runs beside the engine: leave the engine's
+ * readers their cores (e.g. 12 pool threads beside 8 readers on 16 cores;
+ * INTEGRATION.md "The split").  *gpu_count is 0 when no split beats the pool
+ * alone by the 10 % margin, and n_pieces when the GPUs alone are fastest.
+ * out (may be NULL) gets the plan of the split: gpu_s for the GPUs' range,
+ * cpu_s for the pool's, use_gpu = 1 when the GPUs take part. */
 int vx_plan_verify_split(uint64_t n_pieces, uint32_t piece_length, uint64_t total_length, uint32_t cpu_threads,
                          double cpu_thread_rate, uint32_t n_gpus, uint64_t* gpu_first, uint64_t* gpu_count,
                          vx_plan* out);

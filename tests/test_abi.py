@@ -500,13 +500,14 @@ def test_plan_verify_split_host(built):
             assert p.gpu_s > 0 and (count == n or p.cpu_s > 0)
         else:
             assert p.use_gpu == 0 and p.gpu_s == 0 and p.cpu_s == pytest.approx(alone_cpu)
-    # config 5 on the GPU box's 16 threads: the GPU takes most pieces, and the two sides meet; the
-    # measured best split on one box was 770 of 1,387 to the GPU at 64 GiB/s (profiles/r05/split/)
-    first, count, p = _split(1387, 2 * MiB, 2907832320, 16, rate=2.32e9)
-    assert 700 < count < 850 and abs(p.gpu_s - p.cpu_s) < 0.15 * max(p.gpu_s, p.cpu_s)
-    assert 2907832320 / max(p.gpu_s, p.cpu_s) / (1 << 30) == pytest.approx(64, rel=0.1)
-    # the split's GPU share charges its reads to the pool's cores: fewer pieces than an uncharged model gives
-    assert max(p.gpu_s, p.cpu_s) < 0.8 * _plan_g(1387, 2 * MiB, 2907832320, 16, 1).gpu_s
+    # config 5 beside a 12-thread pool (the box's 16 threads less the engine's 8 readers' share): the
+    # GPU takes most pieces and the two sides meet; measured: 763 pieces on the GPU gave 38 / 48 ms
+    # (GPU / pool side), so the balance lies near 800 (profiles/r05/split/)
+    first, count, p = _split(1387, 2 * MiB, 2907832320, 12, rate=2.32e9)
+    assert 750 < count < 850 and abs(p.gpu_s - p.cpu_s) < 0.15 * max(p.gpu_s, p.cpu_s)
+    assert 2907832320 / max(p.gpu_s, p.cpu_s) / (1 << 30) == pytest.approx(61, rel=0.1)
+    # and the split is well below the GPU alone
+    assert max(p.gpu_s, p.cpu_s) < 0.85 * _plan_g(1387, 2 * MiB, 2907832320, 16, 1).gpu_s
     # full node: pool alone
     assert _split(1387, 2 * MiB, 2907832320, 128, g=8)[1] == 0
     # one piece and an empty torrent
@@ -514,7 +515,7 @@ def test_plan_verify_split_host(built):
     from vortex_amd import _lib
     assert _lib.lib().vx_plan_verify_split(10, 0, 10, 16, 2e9, 1, None, None, None) == _lib.VX_EINVAL
     from vortex_amd.hash_pool import plan_verify_split
-    d = plan_verify_split(1387, 2 * MiB, 2907832320, cpu_threads=16, cpu_thread_rate=2.32e9)
+    d = plan_verify_split(1387, 2 * MiB, 2907832320, cpu_threads=12, cpu_thread_rate=2.32e9)
     assert (d["gpu_first"], d["gpu_count"]) == (first, count) and d["use_gpu"] is True
 
 

@@ -270,6 +270,15 @@ def test_reverify_multi_leg_rehearsal(built, gpu):
         assert rm[leg]["value"] > 0 and rm[leg]["cpu_pool"]["value"] > 0
         assert all(len(t) == 2 for t in rm[leg]["rank_traces"])
     _check_plan(rm)
+    _check_split(rm)
+
+
+def _check_split(rm):
+    """The node-level split (bench.multi_split): the planner's GPU tail over the
+    ranks, rank 0's pool on the head, one time per call, every verdict checked."""
+    sp = rm["split"]
+    assert sp["gpu_first"] + sp["gpu_count"] == rm["pieces"] and sp["value"] > 0 and len(sp["s_runs"]) >= 1
+    assert sp["gpu_first"] == sp["plan"]["gpu_first"] and isinstance(sp["beats_both"], bool)
 
 
 def _check_plan(rm):
@@ -305,6 +314,7 @@ def test_reverify_multi_leg_collective_logic_cpu(tmp_path, mode):
         for leg in ("warm", "cold"):
             assert rm[leg]["value"] > 0 and all(len(t) == 2 for t in rm[leg]["rank_traces"])
         _check_plan(rm)
+        _check_split(rm)
     else:
         assert "vx_verify_files_range call failed" in d["error"]
     assert not [p for p in os.listdir(tmp_path) if p.startswith("vx_bench_multi_linuxmint")]

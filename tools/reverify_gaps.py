@@ -8,7 +8,13 @@ Shapes: "<slots>" (the engine's default: copies on the context's copy
 stream) or "<slots>s" (each copy on its slot's stream, round 4's form:
 vx_tuning_verify_copy_stream(ctx, 0), test build).
 
+With --split "io:pool:gpu_frac,...": instead, the split of DESIGN.md §6.6
+(bench.split_call: the engine on the tail with `io` readers while the CPU
+pool restatement verifies the head on `pool` threads), gpu_frac of the pieces
+on the GPU, configs alternating call by call.
+
 usage: python tools/reverify_gaps.py [--reps 5] [--slots 4,4s,6,6s] [--scale 1.0]
+       python tools/reverify_gaps.py --split 8:16:0.55,8:8:0.6,4:12:0.55 [--reps 9]
 """
 import argparse
 import json
@@ -25,10 +31,10 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--slots", default="4,4s,6,6s")
     ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--split", default="")
     a = ap.parse_args()
     import bench
     import oracle
-    from vortex_amd.hash_pool import HashPool
 
     pl = 2097152
     threads = bench.cpu_share()
@@ -37,44 +43,77 @@ def main():
     try:
         total, n, last = bench.write_linuxmint_file(path, a.scale)
         exp = oracle.pool_digest_synth(0x5EED0005, 0, n, pl, last_index=n - 1, last_len=last, threads=threads)
-        shapes = a.slots.split(",")
-        pools = {}
-        for s in shapes:
-            pools[s] = HashPool(pl, slots=int(s.rstrip("s")), slot_bytes=512 << 20, batch_pieces=4096, hooks=True)
-            pools[s].lib.vx_tuning_verify_copy_stream(pools[s]._h, 0 if s.endswith("s") else 1)
-        runs = {s: [] for s in shapes}
-        for s, pool in pools.items():  # warm every context (stages, rows, page cache)
-            got, bad = pool.verify_files([path], [total], pl, exp, io_threads=threads)
-            assert all(got) and bad == 0
-        for _ in range(a.reps):
-            for s, pool in pools.items():
-                t0 = time.perf_counter()
-                got, bad = pool.verify_files([path], [total], pl, exp, io_threads=threads)
-                el = time.perf_counter() - t0
-                assert all(got) and bad == 0
-                rounds = pool.last_verify_rounds()
-                tr = pool.last_verify()
-                g = bench.copy_gaps(rounds)
-                by_slot = {}
-                ns = int(s.rstrip("s"))
-                for k in range(1, len(rounds)):
-                    gap = rounds[k]["copy_start_ms"] - rounds[k - 1]["copy_end_ms"]
-                    by_slot[k % ns] = round(by_slot.get(k % ns, 0.0) + max(0.0, gap), 3)
-                # copies that started within 0.1 ms of the previous round's kernel end
-                after_kernel = sum(1 for k in range(1, len(rounds))
-                                   if 0 <= rounds[k]["copy_start_ms"] - rounds[k - 1]["kernel_end_ms"] < 0.1)
-                runs[s].append({"GiBps": round(total / el / (1 << 30), 2), "copy_busy_frac": round(tr["copy_busy_frac"], 3),
-                                "gap_ms": g["gap_ms"], "by_cause": g["by_cause"], "gap_ms_by_slot": by_slot,
-                                "copy_after_prev_kernel": after_kernel})
-        for s in shapes:
-            r = sorted(runs[s], key=lambda x: x["GiBps"])
-            out["shapes"][f"slots{s}"] = {"median_GiBps": r[len(r) // 2]["GiBps"], "runs": runs[s]}
-        for p in pools.values():
-            p.close()
+        if a.split:
+            out["split"] = split_sweep(a, path, total, n, pl, exp)
+        else:
+            slots_ab(a, out, path, total, n, pl, exp, threads)
     finally:
         if os.path.exists(path):
             os.unlink(path)
     print(json.dumps(out))
+
+
+def slots_ab(a, out, path, total, n, pl, exp, threads):
+    import bench
+    from vortex_amd.hash_pool import HashPool
+
+    shapes = a.slots.split(",")
+    pools = {}
+    for s in shapes:
+        pools[s] = HashPool(pl, slots=int(s.rstrip("s")), slot_bytes=512 << 20, batch_pieces=4096, hooks=True)
+        pools[s].lib.vx_tuning_verify_copy_stream(pools[s]._h, 0 if s.endswith("s") else 1)
+    runs = {s: [] for s in shapes}
+    for s, pool in pools.items():  # warm every context (stages, rows, page cache)
+        got, bad = pool.verify_files([path], [total], pl, exp, io_threads=threads)
+        assert all(got) and bad == 0
+    for _ in range(a.reps):
+        for s, pool in pools.items():
+            t0 = time.perf_counter()
+            got, bad = pool.verify_files([path], [total], pl, exp, io_threads=threads)
+            el = time.perf_counter() - t0
+            assert all(got) and bad == 0
+            rounds = pool.last_verify_rounds()
+            tr = pool.last_verify()
+            g = bench.copy_gaps(rounds)
+            by_slot = {}
+            ns = int(s.rstrip("s"))
+            for k in range(1, len(rounds)):
+                gap = rounds[k]["copy_start_ms"] - rounds[k - 1]["copy_end_ms"]
+                by_slot[k % ns] = round(by_slot.get(k % ns, 0.0) + max(0.0, gap), 3)
+            # copies that started within 0.1 ms of the previous round's kernel end
+            after_kernel = sum(1 for k in range(1, len(rounds))
+                               if 0 <= rounds[k]["copy_start_ms"] - rounds[k - 1]["kernel_end_ms"] < 0.1)
+            runs[s].append({"GiBps": round(total / el / (1 << 30), 2), "copy_busy_frac": round(tr["copy_busy_frac"], 3),
+                            "gap_ms": g["gap_ms"], "by_cause": g["by_cause"], "gap_ms_by_slot": by_slot,
+                            "copy_after_prev_kernel": after_kernel})
+    for s in shapes:
+        r = sorted(runs[s], key=lambda x: x["GiBps"])
+        out["shapes"][f"slots{s}"] = {"median_GiBps": r[len(r) // 2]["GiBps"], "runs": runs[s]}
+    for p in pools.values():
+        p.close()
+
+
+def split_sweep(a, path, total, n, pl, exp):
+    import bench
+    from vortex_amd.hash_pool import HashPool
+
+    cfgs = [tuple(x.split(":")) for x in a.split.split(",")]
+    res = {c: [] for c in cfgs}
+    with HashPool(pl, slots=4, slot_bytes=512 << 20, batch_pieces=4096) as pool:
+        pool.verify_files([path], [total], pl, exp, io_threads=8)
+        for _ in range(a.reps):
+            for c in cfgs:
+                io_t, pool_t, frac = int(c[0]), int(c[1]), float(c[2])
+                first = n - int(round(n * frac))
+                r = bench.split_call(pool, [path], [total], n, pl, exp, first, io_t, pool_t)
+                assert r["ok"]
+                res[c].append((round(r["s"] * 1e3, 2), round(r["gpu_s"] * 1e3, 2), round(r["cpu_s"] * 1e3, 2)))
+    out = {}
+    for c, v in res.items():
+        med = sorted(v)[len(v) // 2]
+        out[":".join(c)] = {"median_GiBps": round(total / (med[0] * 1e-3) / (1 << 30), 2),
+                            "runs_ms_total_gpu_cpu": v}
+    return out
 
 
 if __name__ == "__main__":

@@ -2104,12 +2104,14 @@ constexpr double kChainBlock = 0.76e-6, kPcieRate = 52.0 * (1ull << 30), kSetup 
 constexpr double kOverlapLoss = 0.08, kMargin = 1.1;
 constexpr double kBatchLatency = 1e-3;  // launch, H2D of a small batch, D2H, poll
 // A split runs the GPU side's reads beside the pool's hashing on the same
-// host: each reader byte costs the pool rate / kReadRate of a hashed byte, and
-// the GPU side's bytes move at kSplitLink of the link rate (page-cache reads,
-// stage writes and DMA share host memory with the pool).  Fitted to the warm
-// config-5 split on one box (profiles/r05/split/: GPU side 41 GB/s, pool 0.83
-// of its rate alone, best split 770 of 1,387 pieces to the GPU).
-constexpr double kReadRate = 16.0e9, kSplitLink = 0.74;
+// host.  The pool is sized to leave the engine's readers their cores (the
+// caller passes its size; 12 of 16 threads beside 8 readers measured stable),
+// so it keeps its per-thread rate, while the GPU side's bytes move at
+// kSplitLink of the link rate (page-cache reads, stage writes and the DMA
+// share host memory with the pool's hashing).  Fitted to the warm config-5
+// split (profiles/r05/split/: pool 12 threads at 2.27e9 B/s each, GPU side
+// 41.7 GB/s beside it).
+constexpr double kSplitLink = 0.74;
 
 // The GPU path over `bytes` bytes of pieces piece_length long, over n_gpus links
 // at `link` of the PCIe rate.
@@ -2141,11 +2143,10 @@ int vx_plan_verify_gpus(uint64_t n_pieces, uint32_t piece_length, uint64_t total
 
 // The split of one bulk verify between the GPUs (the tail of the piece range)
 // and the caller's pool (the head), run at once: the GPU side's time is the
-// model above over its bytes; the pool's is its pieces plus the GPU side's
-// reads, which run on the same host cores (one reader byte costs
-// rate / kReadRate of a hashed byte), in rounds of one piece per thread.
-// Every split k = 0..n is scored by the slower side and the fastest wins;
-// unless it beats the pool alone by kMargin the pool keeps everything.
+// model above over its bytes at kSplitLink of the link; the pool's is its
+// pieces in rounds of one piece per thread.  Every split k = 0..n is scored by
+// the slower side and the fastest wins; unless it beats the pool alone by
+// kMargin the pool keeps everything.
 int vx_plan_verify_split(uint64_t n_pieces, uint32_t piece_length, uint64_t total_length, uint32_t cpu_threads,
                          double cpu_thread_rate, uint32_t n_gpus, uint64_t* gpu_first, uint64_t* gpu_count,
                          vx_plan* out) {
@@ -2157,9 +2158,8 @@ int vx_plan_verify_split(uint64_t n_pieces, uint32_t piece_length, uint64_t tota
     const double L = piece_length;
     const double last = n_pieces ? (double)(total_length - (n_pieces - 1) * (uint64_t)piece_length) : 0.0;
     auto gpu_bytes = [&](uint64_t k) { return k ? (double)(k - 1) * L + last : 0.0; };
-    auto cpu_time = [&](uint64_t k) {  // the pool's n - k pieces plus the GPU side's reads
-        const double work = (double)(n_pieces - k) + gpu_bytes(k) / L * (rate / kReadRate);
-        return work > 0 ? std::ceil(work / threads - 1e-9) * (L / rate) : 0.0;
+    auto cpu_time = [&](uint64_t k) {  // the pool's n - k pieces, one per thread per round
+        return k < n_pieces ? std::ceil((double)(n_pieces - k) / threads) * (L / rate) : 0.0;
     };
     vx_plan g{};
     uint64_t best_k = 0;
