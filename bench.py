@@ -705,7 +705,12 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
                   "best_io_threads": best["io_threads"],
                   "planned_value": max(c["value"] for c in planned) if planned else None,
                   "gpu_only": split["gpu_alone"]["value"], "pool_only": split["pool_alone"]["value"],
-                  "beats_both": best["value"] > max(split["gpu_alone"]["value"], split["pool_alone"]["value"]),
+                  # against the better of each side's two figures: in the alternation and in the legs above
+                  "beats_both": best["value"] > max(split["gpu_alone"]["value"], split["pool_alone"]["value"],
+                                                    warm["value"], warm["cpu_pool"]["value"]),
+                  "planned_beats_both": bool(planned) and max(c["value"] for c in planned) > max(
+                      split["gpu_alone"]["value"], split["pool_alone"]["value"], warm["value"],
+                      warm["cpu_pool"]["value"]),
                   "pool_kind": "port",
                   "sample": f"the warm file split at GPU pieces [first, {n}) via vx_verify_files_range while the CPU "
                             f"pool restatement (vortex's par_iter stand-in, 3/4 of the {threads} threads) verifies "

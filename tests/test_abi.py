@@ -502,10 +502,10 @@ def test_plan_verify_split_host(built):
             assert p.use_gpu == 0 and p.gpu_s == 0 and p.cpu_s == pytest.approx(alone_cpu)
     # config 5 beside a 12-thread pool (the box's 16 threads less the engine's 8 readers' share): the
     # GPU takes most pieces and the two sides meet; measured: 763 pieces on the GPU gave 38 / 48 ms
-    # (GPU / pool side), so the balance lies near 800 (profiles/r05/split/)
+    # (GPU / pool side), and 892 the best of three points on two boxes (profiles/r05/split/)
     first, count, p = _split(1387, 2 * MiB, 2907832320, 12, rate=2.32e9)
-    assert 750 < count < 850 and abs(p.gpu_s - p.cpu_s) < 0.15 * max(p.gpu_s, p.cpu_s)
-    assert 2907832320 / max(p.gpu_s, p.cpu_s) / (1 << 30) == pytest.approx(61, rel=0.1)
+    assert 800 < count < 950 and abs(p.gpu_s - p.cpu_s) < 0.15 * max(p.gpu_s, p.cpu_s)
+    assert 2907832320 / max(p.gpu_s, p.cpu_s) / (1 << 30) == pytest.approx(58, rel=0.1)
     # and the split is well below the GPU alone
     assert max(p.gpu_s, p.cpu_s) < 0.85 * _plan_g(1387, 2 * MiB, 2907832320, 16, 1).gpu_s
     # full node: pool alone

@@ -2105,13 +2105,14 @@ constexpr double kOverlapLoss = 0.08, kMargin = 1.1;
 constexpr double kBatchLatency = 1e-3;  // launch, H2D of a small batch, D2H, poll
 // A split runs the GPU side's reads beside the pool's hashing on the same
 // host.  The pool is sized to leave the engine's readers their cores (the
-// caller passes its size; 12 of 16 threads beside 8 readers measured stable),
-// so it keeps its per-thread rate, while the GPU side's bytes move at
-// kSplitLink of the link rate (page-cache reads, stage writes and the DMA
-// share host memory with the pool's hashing).  Fitted to the warm config-5
-// split (profiles/r05/split/: pool 12 threads at 2.27e9 B/s each, GPU side
-// 41.7 GB/s beside it).
-constexpr double kSplitLink = 0.74;
+// caller passes its size; 12 of 16 threads beside 8 readers measured stable);
+// beside the engine it hashes at kSplitPool of its per-thread rate alone, and
+// the GPU side's bytes move at kSplitLink of the link rate (page-cache reads,
+// stage writes and the DMA share host memory with the pool's hashing).  Fitted
+// to the warm config-5 split over three boxes (profiles/r05/split/: GPU side
+// 36-43 GB/s, the 12-thread pool at 0.85-0.98 of its rate alone; the best of
+// three points was the one with the most GPU pieces on two of them).
+constexpr double kSplitLink = 0.74, kSplitPool = 0.85;
 
 // The GPU path over `bytes` bytes of pieces piece_length long, over n_gpus links
 // at `link` of the PCIe rate.
@@ -2159,7 +2160,8 @@ int vx_plan_verify_split(uint64_t n_pieces, uint32_t piece_length, uint64_t tota
     const double last = n_pieces ? (double)(total_length - (n_pieces - 1) * (uint64_t)piece_length) : 0.0;
     auto gpu_bytes = [&](uint64_t k) { return k ? (double)(k - 1) * L + last : 0.0; };
     auto cpu_time = [&](uint64_t k) {  // the pool's n - k pieces, one per thread per round
-        return k < n_pieces ? std::ceil((double)(n_pieces - k) / threads) * (L / rate) : 0.0;
+        if (k >= n_pieces) return 0.0;
+        return std::ceil((double)(n_pieces - k) / threads) * (L / (k ? rate * kSplitPool : rate));
     };
     vx_plan g{};
     uint64_t best_k = 0;
