@@ -291,8 +291,28 @@ def e2e_async(plen: int, n: int = 8192, cpu_thread_GiBps: float | None = None):
     p4 = subprocess.run([exe, str(plen), str(n), f"{4 * total_gib:.6f}", "64", "2"], capture_output=True, text=True,
                         timeout=240)
     d4 = json.loads(p4.stdout.strip().splitlines()[-1]) if p4.returncode == 0 else {"error": p4.stderr[-300:]}
+    # the same burst with refuse_when_full = 1: a submit that finds every slot in flight is refused at
+    # once and the piece goes to a CPU pool (vortex's own, as INTEGRATION.md's call site does; here the
+    # oracle's SHA-NI on cpu_share() - 1 threads, the loop thread being the last): no loop stall, and
+    # the burst is hashed by both sides
+    ot = max(1, cpu_share() - 1)
+    po = subprocess.run([exe, str(plen), str(n), f"{total_gib:.6f}", "64", "2", "0", "4", str(ot)],
+                        capture_output=True, text=True, timeout=240)
+    if po.returncode == 0:
+        do = json.loads(po.stdout.strip().splitlines()[-1])
+        overflow = {"GiBps": do["GiBps"], "pool_threads": ot, "backlog_cap": do.get("backlog_cap"),
+                    "refusals": do["refused"], "cpu_pieces": do["cpu_pieces"], "gpu_pieces": do["polled"],
+                    "mismatched": do["mismatched"], "submit_stall_ms": do["engine"]["submit_stall_ms"],
+                    "blocking_GiBps": d["GiBps"],
+                    "note": "vx_config.refuse_when_full = 1: a refused piece goes to the CPU pool (the CPU pool "
+                            "restatement's SHA-1, vortex's pool stand-in, kind port) while the pool's backlog is "
+                            "under one GPU batch latency of work (vx_plan_verify piece_latency_s / "
+                            "cpu_piece_latency_s x threads), else the loop polls and offers it again; every "
+                            "verdict checked (DESIGN.md §6.5)"}
+    else:
+        overflow = {"error": f"async_probe overflow rc={po.returncode}: {po.stderr[-300:]}"}
     return {"value": d["GiBps"], "unit": "GiB/s", "mismatched": d["mismatched"], "polled": d["polled"],
-            "engine": d.get("engine"),
+            "engine": d.get("engine"), "overflow": overflow,
             "stream_4x": {"GiBps": d4.get("GiBps"), "GiB": round(4 * total_gib, 3), "mismatched": d4.get("mismatched"),
                           "polled": d4.get("polled"), "error": d4.get("error")},
             "paced": paced_leg(plen, cpu_thread_GiBps=cpu_thread_GiBps),

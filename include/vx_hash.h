@@ -99,6 +99,9 @@ typedef struct vx_config {
                                  * 0 (default): as when cached                                                  */
     uint32_t verify_ramp;       /* re-verify: first and last rounds shrink to chunk / 2^(d+1), d = 0..5
                                  * (default 1; 0: no ramp)                                                      */
+    uint32_t refuse_when_full;  /* (ABI 3) async submits: 0 (default) wait for the oldest batch when every slot
+                                 * is in flight; 1: return VX_EBUSY instead, the piece NOT taken, so the event
+                                 * loop never blocks and hands the piece to its own pool (the overflow)      */
 } vx_config;
 
 typedef struct vx_ctx vx_ctx;
@@ -159,7 +162,10 @@ int vx_unregister_host_buffer(vx_ctx* ctx, void* ptr);
  *               through vx_poll as documented there.  If this call's own
  *               batch launch failed part way, the device may still read
  *               `data` until vx_destroy returns.
- * (VX_EBUSY and VX_ENODEV are not returned by submits.) */
+ *   VX_EBUSY    (only with vx_config.refuse_when_full = 1) every slot is in
+ *               flight and the open batch is full: nothing waited, the
+ *               context is unchanged; hash the piece on the caller's pool.
+ * (VX_ENODEV is not returned by submits.) */
 int vx_submit(vx_ctx* ctx, uint64_t tag, const uint8_t* data, uint32_t len, const uint8_t* expected);
 /* Device-resident expected-digest table: upload the
  * torrent's `pieces` string (metadata.pieces, n_pieces x 20 B, the table the
@@ -218,6 +224,7 @@ typedef struct vx_stats {
     uint64_t batch_latency_hist[VX_STATS_HIST]; /* batches per [2^k, 2^(k+1)) us; [0] holds < 2 us, the last bucket everything longer */
     uint64_t zero_copy_slots;     /* (ABI 3) batches hashed straight out of registered host memory (§6.5)  */
     uint64_t zero_copy_loader_slots; /* (ABI 3) ... of them in the three-wave form (slots of < 128 pieces) */
+    uint64_t submits_refused;     /* (ABI 3) async submits refused with VX_EBUSY (refuse_when_full)          */
 } vx_stats;
 int vx_get_stats(const vx_ctx* ctx, vx_stats* out);
 int vx_reset_stats(vx_ctx* ctx);

@@ -37,7 +37,7 @@ def test_completion_layout():
 
     assert ctypes.sizeof(vx_completion) == 32
     assert vx_completion.digest.offset == 9
-    assert ctypes.sizeof(vx_config) == 48
+    assert ctypes.sizeof(vx_config) == 56  # ABI 3: refuse_when_full, padded to 8
 
 
 def test_config_layout(tmp_path):
@@ -78,7 +78,7 @@ def test_stats_layout(tmp_path):
 
 
 @pytest.mark.parametrize("struct,fields", [
-    ("vx_verify_trace", None), ("vx_verify_round", None), ("vx_stats", ("zero_copy_slots", "zero_copy_loader_slots")),
+    ("vx_verify_trace", None), ("vx_verify_round", None), ("vx_stats", ("zero_copy_slots", "zero_copy_loader_slots", "submits_refused")),
     ("vx_plan", None)])
 def test_observability_layouts(tmp_path, struct, fields):
     """ABI 3's observability structs as ctypes have the C layout: size and
@@ -149,10 +149,11 @@ def test_validation_without_gpu(built):
     assert cfg.max_piece_len == 262144 and cfg.slots >= 1 and cfg.batch_pieces >= 1
     assert cfg.slot_bytes >= 262144
     assert (cfg.zero_copy, cfg.direct_io, cfg.batch_chunk, cfg.verify_chunk, cfg.verify_cold_chunk,
-            cfg.verify_ramp) == (1, 1, 65536, 0, 0, 1)
+            cfg.verify_ramp, cfg.refuse_when_full) == (1, 1, 65536, 0, 0, 1, 0)
     h = ctypes.c_void_p()
     # option values outside their ranges are refused before any device is looked at
-    for field, value in (("zero_copy", 2), ("direct_io", 7), ("verify_ramp", 6), ("batch_chunk", 1000),
+    for field, value in (("zero_copy", 2), ("direct_io", 7), ("verify_ramp", 6), ("refuse_when_full", 2),
+                         ("batch_chunk", 1000),
                          ("verify_chunk", 4097), ("verify_cold_chunk", 2048),
                          ("verify_chunk", 2 ** 32 - 4096), ("batch_chunk", (1 << 30) + 4096)):
         badopt = _lib.vx_config()

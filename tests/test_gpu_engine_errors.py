@@ -304,3 +304,48 @@ def test_submit_ownership_every_tag_once(built, gpu, mode):
     else:
         assert list(seen.values()).count("refused") <= 1 and "unfinished" in seen.values()
     pool.close()
+
+
+def test_refuse_when_full_never_blocks(built, gpu):
+    """vx_config.refuse_when_full = 1 (ABI 3): when every slot is in flight
+    and the open batch is full, vx_submit returns VX_EBUSY at once — the
+    piece not taken, the context unchanged — instead of waiting for the
+    oldest batch, so the event loop hands the piece to its own pool.  Every
+    piece is verified exactly once, on whichever side took it; the engine
+    never stalls the submitting thread (submit_stall_ns == 0) and counts
+    its refusals."""
+    from vortex_amd._lib import VX_EBUSY, VxError
+    from vortex_amd.hash_pool import HashPool
+
+    plen, n = 1 << 20, 96
+    bodies = [oracle.gen_piece(0xB5, i, plen) for i in range(n)]
+    want = [hashlib.sha1(b).digest() for b in bodies]
+    bufs = [bytearray(b) for b in bodies]
+    for i in range(0, n, 7):  # some pieces corrupted after their expected digest was taken
+        bufs[i][i % plen] ^= 0x40
+    verdict_truth = [hashlib.sha1(bytes(b)).digest() == w for b, w in zip(bufs, want)]
+    # 2 slots of 8 pieces: 16 pieces fill the pipeline, and 1 MiB chains keep it full for a while
+    with HashPool(plen, slots=2, batch_pieces=8, slot_bytes=8 << 20, refuse_when_full=1) as pool:
+        got, refused = {}, []
+        for i in range(n):
+            try:
+                pool.spawn(i, 7, bufs[i], plen, want[i])
+            except VxError as e:
+                assert e.code == VX_EBUSY and e.refused[0] == i and e.refused[2] is bufs[i]
+                refused.append(i)  # vortex's own pool hashes it (here: hashlib)
+                got[i] = hashlib.sha1(bytes(bufs[i])).digest() == want[i]
+        assert refused, "the pipeline never filled: no refusal to test"
+        pool.drain()
+        for r in pool.try_iter():
+            assert r.index not in got and r.conn_id == 7
+            got[r.index] = r.hash_matched
+        assert sorted(got) == list(range(n))
+        assert [got[i] for i in range(n)] == verdict_truth
+        st = pool.stats()
+        assert st["submits_refused"] == len(refused) and st["submit_stall_ns"] == 0
+        assert st["pieces_completed"] == n - len(refused)
+        # nothing in flight: a submit is taken again
+        pool.spawn(0, 7, bytearray(bodies[0]), plen, want[0])
+        pool.drain()
+        (r,) = pool.try_iter()
+        assert r.hash_matched

@@ -11,13 +11,29 @@
 // line: GiB/s of piece bytes submitted → verdict polled.
 //
 // usage: async_probe <piece_len> [nbuf=1024] [total_GiB=8] [flush_every=64] [registered=1] [slot_MiB=default (0)] [slots=4]
+//                    [overflow_threads=0]
 //   registered: 0 = plain memory (staged), 1 = one registered mmap holding all
 //   buffers, 2 = one mmap per buffer, each registered (vortex's BufferPool,
 //   buf_pool.rs:92-98)
+//   overflow_threads > 0: the context refuses instead of blocking
+//   (vx_config.refuse_when_full = 1) and every refused piece is hashed by a
+//   pool of that many CPU threads (the CPU oracle's SHA-NI SHA-1 standing in
+//   for vortex's rayon pool, as INTEGRATION.md's call site hands it the
+//   piece); the line then also gives each side's share.  The loop gives a
+//   refused piece to the pool only while the pool's backlog is under one GPU
+//   batch latency of work (vx_plan_verify's piece_latency_s over
+//   cpu_piece_latency_s, times the pool's threads); otherwise it polls and
+//   offers the piece to the engine again (both sides full).
 #include <sys/mman.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cmath>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -27,6 +43,56 @@
 #include <vector>
 
 #include "vx_hash.h"
+
+extern "C" void vxo_sha1_backend(const uint8_t* data, size_t len, uint8_t out[20], int backend);  // oracle/
+
+// The overflow pool: refused pieces, hashed and compared on `n` threads.
+struct Overflow {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<uint32_t> q;
+    bool stop = false;
+    std::atomic<uint64_t> done{0}, bad{0};
+    std::vector<std::thread> th;
+    void start(int n, const std::vector<const uint8_t*>& ptrs, uint32_t plen, const std::vector<uint8_t>& dig) {
+        for (int t = 0; t < n; ++t)
+            th.emplace_back([&, plen] {
+                uint8_t d[20];
+                for (;;) {
+                    uint32_t b;
+                    {
+                        std::unique_lock<std::mutex> g(mu);
+                        cv.wait(g, [&] { return stop || !q.empty(); });
+                        if (q.empty()) return;
+                        b = q.front();
+                        q.pop_front();
+                    }
+                    vxo_sha1_backend(ptrs[b], plen, d, 0);
+                    if (std::memcmp(d, &dig[(size_t)b * 20], 20) != 0) bad++;
+                    done++;
+                }
+            });
+    }
+    size_t waiting() {
+        std::lock_guard<std::mutex> g(mu);
+        return q.size();
+    }
+    void push(uint32_t b) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            q.push_back(b);
+        }
+        cv.notify_one();
+    }
+    void finish() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto& t : th) t.join();
+    }
+};
 
 static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
@@ -51,6 +117,8 @@ int main(int argc, char** argv) {
         cfg.batch_pieces = (uint32_t)std::min<uint64_t>(65536, cfg.slot_bytes / ((plen + 255) / 256 * 256));
     }
     if (argc > 7) cfg.slots = (uint32_t)std::atoi(argv[7]);  // batch slots (default 4)
+    const int overflow_threads = argc > 8 ? std::atoi(argv[8]) : 0;
+    cfg.refuse_when_full = overflow_threads > 0 ? 1 : 0;
     vx_ctx* ctx = nullptr;
     if (int rc = vx_create(&cfg, &ctx)) {
         std::fprintf(stderr, "vx_create: %d %s\n", rc, vx_last_error());
@@ -112,7 +180,13 @@ int main(int argc, char** argv) {
     for (int pass = 0; pass < 4; ++pass) {
         std::shuffle(order.begin(), order.end(), rng);
         for (uint32_t b : order) {
-            if (vx_submit(ctx, b, ptrs[b], plen, &digests[(size_t)b * 20])) return 1;
+            int rc;
+            while ((rc = vx_submit(ctx, b, ptrs[b], plen, &digests[(size_t)b * 20])) == VX_EBUSY)
+                if (poll()) return 1;  // refuse_when_full: the warm-up waits for the GPU itself
+            if (rc) {
+                std::fprintf(stderr, "warm-up vx_submit: %d %s\n", rc, vx_last_error());
+                return 1;
+            }
             if (++sent % flush_every == 0 && (vx_flush(ctx) || poll())) return 1;
         }
     }
@@ -120,13 +194,35 @@ int main(int argc, char** argv) {
     polled = 0;
     bad = 0;
     sent = 0;
+    Overflow ov;
+    size_t backlog_cap = 0;
+    if (overflow_threads > 0) {
+        ov.start(overflow_threads, ptrs, plen, digests);
+        vx_plan pl{};
+        vx_plan_verify(1, plen, plen, (uint32_t)overflow_threads, 0.0, &pl);
+        backlog_cap = (size_t)overflow_threads *
+                      (size_t)std::max(1.0, std::round(pl.piece_latency_s / std::max(1e-9, pl.cpu_piece_latency_s)));
+    }
+    uint64_t refused = 0, to_cpu = 0;
     vx_reset_stats(ctx);  // the engine's own view of the timed region (vx_get_stats)
     const double t0 = now_s();
     while (sent < total) {
         std::shuffle(order.begin(), order.end(), rng);
         for (uint32_t b : order) {
             if (sent == total) break;
-            if (int rc = vx_submit(ctx, b, ptrs[b], plen, &digests[(size_t)b * 20])) {
+            int rc;
+            while ((rc = vx_submit(ctx, b, ptrs[b], plen, &digests[(size_t)b * 20])) == VX_EBUSY &&
+                   overflow_threads > 0) {
+                ++refused;
+                if (ov.waiting() < backlog_cap) {  // not taken: the loop's own pool hashes it
+                    ov.push(b);
+                    rc = 0;
+                    ++to_cpu;
+                    break;
+                }
+                if (poll()) return 1;  // both sides full: harvest and offer it to the engine again
+            }
+            if (rc) {
                 std::fprintf(stderr, "vx_submit: %d %s\n", rc, vx_last_error());
                 return 1;
             }
@@ -136,7 +232,9 @@ int main(int argc, char** argv) {
         }
     }
     if (vx_drain(ctx, 0) || poll()) return 1;
+    if (overflow_threads > 0) ov.finish();
     const double el = now_s() - t0;
+    bad += ov.bad.load();
     vx_stats st{};
     vx_get_stats(ctx, &st);
     // median batch latency from the log2 histogram: the bucket holding the middle batch
@@ -154,15 +252,17 @@ int main(int argc, char** argv) {
     vx_destroy(ctx);
     for (uint8_t* m : maps) munmap(m, map_bytes);
     std::printf("{\"piece_len\": %u, \"pieces\": %llu, \"registered\": %d, \"flush_every\": %u, \"GiBps\": %.3f, "
+                "\"overflow_threads\": %d, \"backlog_cap\": %zu, \"refused\": %llu, \"cpu_pieces\": %llu, "
                 "\"mismatched\": %llu, \"polled\": %llu, \"engine\": {\"batches\": %llu, \"pieces_completed\": %llu, "
                 "\"gather_tiles\": %llu, \"staged_bytes\": %llu, \"submit_stall_ms\": %.3f, "
                 "\"batch_latency_mean_ms\": %.3f, \"batch_latency_max_ms\": %.3f, "
                 "\"batch_latency_median_bucket_ms\": [%.3f, %.3f]}}\n",
                 plen, (unsigned long long)total, registered, flush_every,
-                (double)total * plen / el / (1 << 30), (unsigned long long)bad, (unsigned long long)polled,
+                (double)total * plen / el / (1 << 30), overflow_threads, backlog_cap, (unsigned long long)refused,
+                (unsigned long long)ov.done.load(), (unsigned long long)bad, (unsigned long long)polled,
                 (unsigned long long)st.batches, (unsigned long long)st.pieces_completed,
                 (unsigned long long)st.gather_tiles, (unsigned long long)st.staged_bytes, st.submit_stall_ns * 1e-6,
                 st.batch_latency_count ? st.batch_latency_sum_us * 1e-3 / st.batch_latency_count : 0.0,
                 st.batch_latency_max_us * 1e-3, (double)(med ? 1ull << med : 0) * 1e-3, (double)(2ull << med) * 1e-3);
-    return bad == 0 && polled == total ? 0 : 3;
+    return bad == 0 && polled + ov.done.load() == total ? 0 : 3;
 }

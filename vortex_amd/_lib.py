@@ -72,7 +72,8 @@ class vx_completion(ctypes.Structure):
 ABI_VERSION = 3
 
 # vx_config fields a caller may set beyond the pool geometry (ABI 2; include/vx_hash.h)
-CONFIG_OPTIONS = ("zero_copy", "direct_io", "batch_chunk", "verify_chunk", "verify_cold_chunk", "verify_ramp")
+CONFIG_OPTIONS = ("zero_copy", "direct_io", "batch_chunk", "verify_chunk", "verify_cold_chunk", "verify_ramp",
+                  "refuse_when_full")
 
 
 class vx_config(ctypes.Structure):
@@ -95,7 +96,7 @@ class vx_stats(ctypes.Structure):
         "pieces_completed", "pieces_mismatched", "bytes_completed", "batches", "chunk_rounds", "gather_tiles",
         "staged_bytes", "io_errors", "submit_stall_ns", "batch_latency_count", "batch_latency_sum_us",
         "batch_latency_max_us")] + [("batch_latency_hist", ctypes.c_uint64 * VX_STATS_HIST)] + [
-        (name, ctypes.c_uint64) for name in ("zero_copy_slots", "zero_copy_loader_slots")]
+        (name, ctypes.c_uint64) for name in ("zero_copy_slots", "zero_copy_loader_slots", "submits_refused")]
 
 
 class vx_verify_trace(ctypes.Structure):

@@ -621,9 +621,11 @@ bool may_launch_now(const vx_ctx* c) {
     return inflight < std::max(1, (int)c->slots.size() - 1);
 }
 
-int acquire_filling(vx_ctx* c) {
+// may_wait = false (an async submit with refuse_when_full): harvest what has
+// finished without blocking, and if no slot is free then, VX_EBUSY.
+int acquire_filling(vx_ctx* c, bool may_wait = true) {
     if (c->filling >= 0) return c->filling;
-    for (;;) {
+    for (int attempt = 0;; ++attempt) {
         for (int i = 0; i < (int)c->slots.size(); ++i) {
             if (c->slots[i].state == Slot::FREE) {
                 reset_fill(c->slots[i]);
@@ -631,6 +633,14 @@ int acquire_filling(vx_ctx* c) {
                 c->filling = i;
                 return i;
             }
+        }
+        if (!may_wait) {
+            if (attempt > 0) {
+                c->stats.submits_refused++;
+                return fail(VX_EBUSY, "vx_submit: every slot in flight (refuse_when_full)");
+            }
+            if (int rc = reap(c, /*block_oldest=*/false)) return rc;
+            continue;
         }
         const auto t0 = std::chrono::steady_clock::now();
         int rc = reap(c, /*block_oldest=*/true);
@@ -652,7 +662,8 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
         return fail(VX_ENOMEM, "vx_submit: injected failure (vx_tuning_fail_submit_after)");
 #endif
     const bool table = piece_row >= 0;
-    int si = acquire_filling(c);
+    const bool may_wait = !c->cfg.refuse_when_full || c->bulk;  // host batches always wait
+    int si = acquire_filling(c, may_wait);
     if (si < 0) return si;
     Slot* s = &c->slots[si];
     uint64_t off = align_up(s->bytes, kAlign);
@@ -660,7 +671,7 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
     if (s->n == s->cap || off + len > s->arena_cap || (s->n && s->use_table != table)) {
         int rc = launch_slot(c, si);
         if (rc) return rc;
-        si = acquire_filling(c);
+        si = acquire_filling(c, may_wait);
         if (si < 0) return si;
         s = &c->slots[si];
         off = 0;
@@ -795,6 +806,7 @@ void vx_config_default(vx_config* cfg, uint32_t max_piece_len) {
     cfg->verify_chunk = 0;         // per call: verify_chunk_for
     cfg->verify_cold_chunk = 0;
     cfg->verify_ramp = 1;
+    cfg->refuse_when_full = 0;
 }
 
 int vx_create(const vx_config* cfg, vx_ctx** out) {
@@ -803,8 +815,8 @@ int vx_create(const vx_config* cfg, vx_ctx** out) {
     if (cfg->max_piece_len == 0 || cfg->slots == 0 || cfg->batch_pieces == 0)
         return fail(VX_EINVAL, "vx_create: max_piece_len, slots and batch_pieces must be > 0");
     if (cfg->slot_bytes < cfg->max_piece_len) return fail(VX_EINVAL, "vx_create: slot_bytes < max_piece_len");
-    if (cfg->zero_copy > 1 || cfg->direct_io > 1)
-        return fail(VX_EINVAL, "vx_create: zero_copy and direct_io are 0 or 1");
+    if (cfg->zero_copy > 1 || cfg->direct_io > 1 || cfg->refuse_when_full > 1)
+        return fail(VX_EINVAL, "vx_create: zero_copy, direct_io and refuse_when_full are 0 or 1");
     if (cfg->verify_ramp > 5) return fail(VX_EINVAL, "vx_create: verify_ramp must be 0..5");
     if ((cfg->batch_chunk && (cfg->batch_chunk < 4096 || cfg->batch_chunk % 4096)) ||
         (cfg->verify_chunk && (cfg->verify_chunk < 4096 || cfg->verify_chunk % 4096)) ||
