@@ -697,15 +697,22 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
     def record(leg):
         gpu_t, cpu_t, traces, resident = legs[leg]
         g, c = sorted(gpu_t)[len(gpu_t) // 2], sorted(cpu_t)[len(cpu_t) // 2]
-        # what bound this box's calls: the H2D copies busy nearly
-        # all the time = PCIe; copies waiting on the readers = the host's reads
-        cb = sorted(t["copy_busy_frac"] for t in traces if t.get("copy_busy_frac") is not None)
-        cbm = cb[len(cb) // 2] if cb else None
-        bound = None if cbm is None else (
-            "pcie (H2D copies busy >= 0.95 of the call)" if cbm >= 0.95 else
-            f"host reads (H2D copies busy {cbm:.2f}: waiting on {'the disk' if leg == 'cold' else 'page-cache reads'})")
         # the median call's copy-engine gaps by cause (its full timeline stays in gpu_traces)
         med_trace = traces[sorted(range(len(gpu_t)), key=lambda i: gpu_t[i])[len(gpu_t) // 2]]
+        # what bound this box's calls: the H2D copies busy nearly all
+        # the time = PCIe; otherwise the cause that left the copy engine idle longest in
+        # the median call's round timeline (the reads, the hand-off, or the device)
+        cb = sorted(t["copy_busy_frac"] for t in traces if t.get("copy_busy_frac") is not None)
+        cbm = cb[len(cb) // 2] if cb else None
+        causes = (med_trace.get("copy_gaps") or {}).get("by_cause") or {}
+        top = max(causes, key=causes.get) if causes else "read"
+        what = {"read": f"host reads (waiting on {'the disk' if leg == 'cold' else 'page-cache reads'})",
+                "hand-off": "the hand-off (reads done, round enqueued late)",
+                "device": "the device (copies enqueued in time, started late)"}[top]
+        bound = None if cbm is None else (
+            "pcie (H2D copies busy >= 0.95 of the call)" if cbm >= 0.95 else
+            f"{what}; H2D copies busy {cbm:.2f}, median call's idle copy engine {causes.get(top, 0):.1f} ms by this "
+            f"cause")
         for t in traces:  # one full timeline (the median call's) is enough for the record
             if t is not med_trace:
                 t.pop("timeline", None)
