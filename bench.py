@@ -974,10 +974,14 @@ def multi_split(rank, world, pool, path, total, n, exp, io_threads, ncpu, cpu, a
         res = {}
 
         def head():
-            t0 = time.perf_counter()
-            res["head"] = oracle.pool_verify_files([path], [total], pl, exp[:20 * first],
-                                                   threads=max(1, ncpu * 3 // 4))
-            res["head_s"] = time.perf_counter() - t0
+            try:
+                t0 = time.perf_counter()
+                res["head"] = oracle.pool_verify_files([path], [total], pl, exp[:20 * first],
+                                                       threads=max(1, ncpu * 3 // 4))
+                res["head_s"] = time.perf_counter() - t0
+            except Exception as e:  # noqa: BLE001  (a failed head is a wrong-verdict run, below)
+                log(f"split: the CPU pool's head failed: {type(e).__name__}: {e}")
+                res["head"] = []
 
         th = threading.Thread(target=head) if rank == 0 and first else None
         ok = True
