@@ -46,11 +46,12 @@ void vx_tuning_fail_submit_after(struct vx_ctx* ctx, int64_t k);
  * launch fails as a device error does (VX_EDEVICE, the context turns sticky):
  * the recovery path of INTEGRATION.md "Device failure".  k < 0 turns it off. */
 void vx_tuning_fail_launch_after(struct vx_ctx* ctx, int64_t k);
-/* A/B of the file re-verify's copy placement: on = 1 (the
- * default) puts every chunk round's H2D on the context's one high-priority
- * copy stream; 0 puts each on its slot's stream behind a host wait for the
- * previous round's copy (round 4's form). */
-void vx_tuning_verify_copy_stream(struct vx_ctx* ctx, int on);
+/* A/B of the file re-verify's copy placement: mode 1 (the
+ * default) puts every chunk round's data H2D on the context's one
+ * high-priority copy stream and its lane table on the slot's stream; 0 puts
+ * both on the slot's stream behind a host wait for the previous round's copy
+ * (round 4's form). */
+void vx_tuning_verify_copy_stream(struct vx_ctx* ctx, int mode);
 /* The kernel vx_sha1_device_ragged_hint runs for a batch of n pieces whose
  * longest is max_len bytes, total_len bytes in all: 1 = lane, 2 = split,
  * 5 = split with one pair per CU (host-only). */

@@ -4,9 +4,11 @@ vx_verify_files over the linux-mint-geometry file for several context shapes,
 alternating, each call's round timeline (vx_last_verify_rounds) reduced by
 bench.copy_gaps to gaps by cause and by slot.  Prints one JSON line.
 
-Shapes: "<slots>" (the engine's default: copies on the context's copy
-stream) or "<slots>s" (each copy on its slot's stream, round 4's form:
-vx_tuning_verify_copy_stream(ctx, 0), test build).
+Shapes: "<slots>" (the engine's default: data copies on the context's copy
+stream, lane tables on the slot streams) or "<slots>s" (each copy on its
+slot's stream, round 4's form): vx_tuning_verify_copy_stream(ctx, 1 / 0),
+test build.  (Round 5 also measured the tables on the copy stream, and a
+normal-priority copy stream: EXPERIMENTS.md §6.3.)
 
 With --split "io:pool:gpu_frac,...": instead, the split of DESIGN.md §6.6
 (bench.split_call: the engine on the tail with `io` readers while the CPU
@@ -32,16 +34,32 @@ def main():
     ap.add_argument("--slots", default="4,4s,6,6s")
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--split", default="")
+    ap.add_argument("--geometry", default="", help="N:MiB = N pieces of MiB each instead of linux-mint's")
     a = ap.parse_args()
     import bench
     import oracle
 
     pl = 2097152
+    if a.geometry:
+        pl = int(a.geometry.split(":")[1]) << 20
     threads = bench.cpu_share()
     path = os.path.join(bench.reverify_dir(), f"vx_gaps_{os.getpid()}.iso")
     out = {"threads": threads, "shapes": {}}
     try:
-        total, n, last = bench.write_linuxmint_file(path, a.scale)
+        if a.geometry:
+            n = int(a.geometry.split(":")[0])
+            total, last = n * pl, pl
+            import ctypes
+
+            buf = ctypes.create_string_buffer(pl)
+            with open(path, "wb") as f:
+                for i in range(n):
+                    oracle.lib().vxo_gen_piece(0x5EED0005, i, pl, 0, buf)
+                    f.write(buf.raw)
+                f.flush()
+                os.fsync(f.fileno())
+        else:
+            total, n, last = bench.write_linuxmint_file(path, a.scale)
         exp = oracle.pool_digest_synth(0x5EED0005, 0, n, pl, last_index=n - 1, last_len=last, threads=threads)
         if a.split:
             out["split"] = split_sweep(a, path, total, n, pl, exp)
@@ -84,6 +102,9 @@ def slots_ab(a, out, path, total, n, pl, exp, threads):
             after_kernel = sum(1 for k in range(1, len(rounds))
                                if 0 <= rounds[k]["copy_start_ms"] - rounds[k - 1]["kernel_end_ms"] < 0.1)
             runs[s].append({"GiBps": round(total / el / (1 << 30), 2), "copy_busy_frac": round(tr["copy_busy_frac"], 3),
+                            "copy_GiBps": round(tr["copy_GiBps"], 2), "read_GiBps": round(tr["read_GiBps"], 2),
+                            "wall_ms": round(tr["wall_ms"], 2), "copy_span_ms": round(tr["copy_span_ms"], 2),
+                            "first_copy_ms": g["first_copy_start_ms"],
                             "gap_ms": g["gap_ms"], "by_cause": g["by_cause"], "gap_ms_by_slot": by_slot,
                             "copy_after_prev_kernel": after_kernel})
     for s in shapes:

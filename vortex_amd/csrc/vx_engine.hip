@@ -1191,6 +1191,11 @@ struct ChunkPipe {
     // slot's kernel there waited for that kernel: 5-7 ms of idle PCIe per
     // warm linux-mint call with 4-6 slots (profiles/r05/gaps/).
     hipStream_t cs = nullptr;
+    // Set by a copy_data that records a timing event right after its copy on
+    // the copy stream: the slot's stream waits on that one instead of a
+    // separate `copied` marker (each marker between two copies on one stream
+    // costs the copy engine ~15 us; 36 rounds of 8 MiB pieces add up).
+    hipEvent_t copy_end = nullptr;
 
     explicit ChunkPipe(vx_ctx* ctx) : c(ctx) {}
 
@@ -1311,22 +1316,29 @@ struct ChunkPipe {
         if (!rc) rc = reap(c, false);
         return rc;
     }
-    // round() with the copies on the copy stream: data, then the lane table,
-    // then `copied`; the slot's stream waits for it and runs the kernel.  The
-    // copies stay in launch order (one stream), with no host wait between
-    // them; the slot is reused only after its `done` (free_slot), so no copy
-    // overwrites a stage or arena a kernel still reads.
+    // round() with the data copies on the copy stream, then `copied`; the
+    // slot's stream takes the round's small lane table, waits for `copied`
+    // and runs the kernel.  The data copies stay in launch order (one stream)
+    // back to back, with no host wait and no small table copy between them
+    // (on the copy stream each table added ~70 us to every round: 2.6 ms of
+    // a 1,024 x 8 MiB call, profiles/r05/gaps/).  A table behind an aliased
+    // slot's kernel only waits where the kernel waits anyway (the previous
+    // round's state).  The slot is reused only after its `done` (free_slot),
+    // so no copy overwrites a stage or arena a kernel still reads.
     template <class F>
     int round_cs(int si, uint32_t m, bool continues, F&& copy_data) {
         Slot& s = c->slots[si];
         hipStream_t st = s.stream;
         const size_t meta = (size_t)(reinterpret_cast<const uint8_t*>(s.h_pidx + m) - reinterpret_cast<const uint8_t*>(s.h_offsets));
+        copy_end = nullptr;
         int rc = copy_data(s, cs);
-        if (!rc && hipMemcpyAsync(s.d_offsets, s.h_offsets, meta, hipMemcpyHostToDevice, cs) != hipSuccess)
+        hipEvent_t copied = copy_end ? copy_end : s.copied;
+        if (!rc && copied == s.copied && hipEventRecord(s.copied, cs) != hipSuccess)
+            rc = fail(VX_EDEVICE, "chunk round: event failed");
+        if (!rc && hipMemcpyAsync(s.d_offsets, s.h_offsets, meta, hipMemcpyHostToDevice, st) != hipSuccess)
             rc = fail(VX_EDEVICE, "chunk round: H2D failed");
-        if (!rc && hipEventRecord(s.copied, cs) != hipSuccess) rc = fail(VX_EDEVICE, "chunk round: event failed");
         mark_launched(c, si);
-        if (!rc && hipStreamWaitEvent(st, s.copied, 0) != hipSuccess)
+        if (!rc && hipStreamWaitEvent(st, copied, 0) != hipSuccess)
             rc = fail(VX_EDEVICE, "chunk round: stream wait failed");
         if (!rc && continues && have_prev && hipStreamWaitEvent(st, prev_kernel, 0) != hipSuccess)
             rc = fail(VX_EDEVICE, "chunk round: stream wait failed");
@@ -1552,6 +1564,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
                 return fail(VX_EDEVICE, "vx_verify_files: chunk H2D failed");
             if (ev && hipEventRecord(c->copy_ev[3 * timed + 1], st) == hipSuccess) {  // timing is best effort
                 timed_bytes.push_back(sl.bytes);
+                cp.copy_end = c->copy_ev[3 * timed + 1];  // doubles as the round's `copied` (copy stream)
                 ev_k = (long)timed++;
             }
             return 0;
@@ -2247,8 +2260,8 @@ void vx_tuning_fail_submit_after(vx_ctx* c, int64_t k) {
 void vx_tuning_fail_launch_after(vx_ctx* c, int64_t k) {
     if (c) c->fail_launch_after = k < 0 ? -1 : k;
 }
-void vx_tuning_verify_copy_stream(vx_ctx* c, int on) {
-    if (c) c->verify_copy_stream = on ? 1 : 0;
+void vx_tuning_verify_copy_stream(vx_ctx* c, int mode) {
+    if (c) c->verify_copy_stream = mode ? 1 : 0;
 }
 #endif
 size_t vx_tuning_chunk_schedule(uint64_t L, uint64_t C, int head, int tail, uint64_t* out, size_t max) {
