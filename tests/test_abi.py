@@ -542,3 +542,25 @@ def test_plan_verify_split_on_measured_grid(built):
         cpu_side = c_s * first / n
         assert max(gpu_side, cpu_side) <= min(g_s, c_s) * 1.0001, pt
     assert seen >= 5
+
+
+def test_plan_verify_decisions_on_the_round5_grid(built):
+    """The same decisions on the crossover grid re-measured on round 5's engine
+    (profiles/r05/crossover/grid.json, another box): wherever the measured GPU
+    and CPU-pool times differ by more than 10 % the planner picks the measured
+    winner, and the chain-bound points (the GPU side's floor) are predicted
+    within 10 %."""
+    import json
+
+    with open(os.path.join(ROOT, "profiles", "r05", "crossover", "grid.json")) as f:
+        grid = json.load(f)
+    MiB = 1 << 20
+    assert len(grid["points"]) >= 20
+    for pt in grid["points"]:
+        L = pt["piece_MiB"] * MiB
+        rc, p = _plan(pt["n"], L, pt["n"] * L, threads=grid["threads"])
+        assert rc == 0
+        if max(pt["gpu_s"], pt["cpu_s"]) > 1.1 * min(pt["gpu_s"], pt["cpu_s"]):
+            assert p.use_gpu == (pt["winner"] == "gpu"), pt
+        if pt["n"] <= 256:  # chain-bound: one lane's chain, whatever the host
+            assert abs(p.gpu_s / pt["gpu_s"] - 1) < 0.10, (pt, p.gpu_s)
