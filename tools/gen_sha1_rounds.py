@@ -4,9 +4,9 @@ stream with a fixed issue order and register map, and check it.
 
 Why: a lone wave (the split kernel's consumer) runs hipcc's
 round code at ~4.5 cycles per VALU against a 4-cycle issue floor
-(tools/native/rounds_sched_probe.hip), and hipcc decides both the order and
-the registers.  This emits the rounds with both fixed, so a probe (and, if it
-pays, the kernel) can run exactly this stream.
+(EXPERIMENTS.md, round 2), and hipcc decides both the order and the
+registers.  This emits the rounds with both fixed, and `--consumer` writes the
+split kernels' consumer loop (vortex_amd/csrc/sha1_consumer_asm.inc) from them.
 
 Dataflow (FIPS 180-4 round t: T = rotl5(a) + f(b, c, d) + e + K + W[t];
 e = d; d = c; c = rotl30(b); b = a; a = T).  With A_t = T of round t:
@@ -116,99 +116,47 @@ def consumer_regs(wbase: int) -> Regs:
                 f=["v79", "v80"], r="v81", k=["s20", "s21", "s22", "s23"])
 
 
-ADDR = "v87"  # burst2: LDS address of the next block's slot (base + s25)
+def _read(dst_base: int, q: int, slot: int) -> str:
+    """ds_read of quad q of ring slot `slot`, addressed from %5 (lds.w[0][0][lane])."""
+    return f"ds_read_b128 v[{dst_base + 4 * q}:{dst_base + 4 * q + 3}], %5 offset:{slot * SLOT_BYTES + q * QUAD_BYTES}"
 
 
-def _read(dst_base: int, q: int, slot: int, addr: str = "%5") -> str:
-    """ds_read of quad q of ring slot `slot`.  Slots 0-2 are addressed from %5
-    (lds.w[0][0][lane]), slots 3-5 of the 6-slot ring from %9 (lds.w[3][0][lane])
-    so every offset fits the 16-bit field."""
-    if addr == "%5" and slot >= 3:
-        addr, slot = "%9", slot - 3
-    off = (slot * SLOT_BYTES if addr in ("%5", "%9") else 0) + q * QUAD_BYTES
-    return f"ds_read_b128 v[{dst_base + 4 * q}:{dst_base + 4 * q + 3}], {addr} offset:{off}"
-
-
-def _block(R: Regs, mode: str, next_slot: int, next_base: int):
-    """One block: the 80 rounds + feed-forward on R's word registers, with the
-    next block's 20 ring reads into next_base placed per `mode`."""
+def _block(R: Regs, next_slot: int, next_base: int):
+    """One block: the next block's 20 ring reads into next_base (burst), then
+    the 80 rounds + feed-forward on R's word registers, then lgkmcnt(0)."""
     ins, final = rounds(R)
-    body = emit(ins, final, R.h, feed_forward=False).splitlines()
-    out = []
-    # probe-only placements (pair_probe, DESIGN.md §3.2.1): reads at rounds given by `at`
-    at = {"none": {}, "split2": {0: range(0, 10), 40: range(10, 20)},
-          "split4": {0: range(0, 5), 20: range(5, 10), 40: range(10, 15), 60: range(15, 20)},
-          "spread4": {4 * q: [q] for q in range(20)}, "late": {60: range(20)}}.get(mode)
-    if mode == "burst":
-        out += [_read(next_base, q, next_slot) for q in range(20)]
-    elif at is not None:
-        pass
-    elif mode == "burst2":
-        out += [f"v_add_u32_e64 {ADDR}, s25, %5"] + [_read(next_base, q, 0, ADDR) for q in range(20)]
-    else:
-        out += ["s_waitcnt lgkmcnt(15)", "s_nop 0"]
-    out += body[0:3]  # prologue
-    for t in range(80):
-        n_t = 5 if t < 79 else 2
-        chunk = body[3 + 5 * t: 3 + 5 * t + n_t]
-        if mode == "refill" and t == 16:
-            out += ["s_waitcnt lgkmcnt(4)", "s_nop 0"]
-        out.append(chunk[0])
-        if at is not None and t in at:
-            out += [_read(next_base, q, next_slot) for q in at[t]]
-        if mode == "refill" and t < 79 and (t - 2) % 4 == 0:  # X_{4q+3} done: quad q is free
-            out.append(_read(next_base, (t - 2) // 4, next_slot))
-        if mode == "spread" and t < 20:  # one read per round over the first 20 rounds
-            out.append(_read(next_base, t, next_slot))
-        out += chunk[1:]
+    out = [_read(next_base, q, next_slot) for q in range(20)]
+    out += emit(ins, final, R.h, feed_forward=False).splitlines()
     out += [f"v_add_u32_e64 {h}, {h}, {f}" for h, f in zip(R.h, final)]
-    if mode in ("burst", "burst2", "spread") or at is not None:
-        out += ["s_waitcnt lgkmcnt(0)", "s_nop 0"]
-    return out
+    return out + ["s_waitcnt lgkmcnt(0)", "s_nop 0"]
 
 
-def consumer_asm(select: bool, mode: str = "burst", slots: int = 3) -> str:
+def consumer_asm(select: bool) -> str:
     """The whole consumer of sha1_*split_kernel as one asm body.  Operands:
     %0-%4 state h0-h4 ("+v"), %5 LDS byte address of lds.w[0][0][lane] ("v"),
     %6 nb_wave ("s"), %7 b1 ("s"), %8 the lane's nb ("v"; used only when
-    `select`), and with slots = 6 %9 the address of lds.w[3][0][lane].
+    `select`).
 
-    Barriers, slots = 3: none when nb_wave == 0, else one before block 0 and
-    one after every block (1 + nb_wave, matching the producer's publish /
-    producer_done).  slots = 6: one before block 0 and one after every PAIR of
-    blocks (the last pair may hold one block): 1 + ceil(nb_wave / 2); the
-    producer publishes pairs 0 and 1 before the first barrier and pair q + 1
-    before barrier q, and overwrites pair q's slots only after barrier q + 1.
-    Ring reads of block b+1 (slot (b+1) % 3):
-      refill  during block b, quad q right after its last use (X_{4q+3},
-              round 4q+2), into the same registers: one word set; waits
-              lgkmcnt(15) at a block's start and lgkmcnt(4) at round 16;
-      burst   all 20 at the top of block b into the other of two word sets,
-              lgkmcnt(0) at its end (the kernel's: 3-7 % faster than hipcc's
-              consumer of the same form, while refill was 1.5-3.5 % slower
-              and one read per round over rounds 0-19 5-9 % slower;
-              profiles/r02/consumer_asm/);
-      burst2  as burst with a 2-block loop: the next slot's address is
-              base + s25 (one v_add and three SALU per block) instead of
-              immediate offsets, so the loop is a third of the code;
-      spread  as burst, one read per round over rounds 0-19.
+    Barriers: none when nb_wave == 0, else one before block 0 and one after
+    every block (1 + nb_wave, matching the producer's publish / producer_done).
+    Ring reads of block b+1 (slot (b+1) % 3): all 20 at the top of block b into
+    the other of two word sets, lgkmcnt(0) at its end ("burst": 3-7 % faster
+    than hipcc's consumer of the same form; a per-quad refill was 1.5-3.5 %
+    slower and one read per round 5-9 % slower, profiles/r02/consumer_asm/;
+    the 6-slot ring and an LDS flag handshake were no faster, EXPERIMENTS.md).
     Blocks b >= b1 (ragged phase 2, `select`) keep the new state only in
     lanes with b < nb (v_cndmask on v_cmp b < nb).  Hot-path instructions are
     8 bytes and scalar ones come in pairs, so bodies stay 8-byte aligned
     (DESIGN.md §3.6)."""
-    # slots cycle by 3 (or 6), word sets by 2; burst2 addresses the slot through s25
-    unroll = {"refill": 3, "burst2": 2}.get(mode, 6)
-    assert slots == 3 or (slots == 6 and mode == "burst")
     L = [f"v_mov_b32_e64 v{H0 + i}, %{i}" for i in range(5)]
     L += ["s_mov_b32 s20, 0x5a827999", "s_mov_b32 s21, 0x6ed9eba1", "s_mov_b32 s22, 0x8f1bbcdc",
           "s_mov_b32 s23, 0xca62c1d6", "s_mov_b32 s24, 0", f"s_mov_b32 s25, {SLOT_BYTES}",
           "s_cmp_eq_u32 %6, 0", "s_cbranch_scc1 .Lvx_end%=", "s_barrier"]
     L += [_read(WA, q, 0) for q in range(20)]
     L += ["s_waitcnt lgkmcnt(0)", "s_nop 0", ".p2align 5", ".Lvx_loop%=:"]
-    for k in range(unroll):
-        cur = WA if (mode == "refill" or k % 2 == 0) else WB
-        nxt = WA if mode == "refill" else (WB if cur == WA else WA)
-        body = _block(consumer_regs(cur), mode, (k + 1) % slots, nxt)
+    for k in range(6):  # slots cycle by 3, word sets by 2
+        cur, nxt = (WA, WB) if k % 2 == 0 else (WB, WA)
+        body = _block(consumer_regs(cur), (k + 1) % 3, nxt)
         if select:
             L += ["s_cmp_lt_u32 s24, %7", f"s_cbranch_scc0 .Lvx_sel{k}_%=", ".p2align 3"]
             L += body
@@ -220,126 +168,34 @@ def consumer_asm(select: bool, mode: str = "burst", slots: int = 3) -> str:
             L += [".p2align 3", f".Lvx_done{k}_%=:"]
         else:
             L += body
-        if slots == 6 and k % 2 == 0:  # first block of a pair: a barrier only if it is the last block
-            L += ["s_add_u32 s24, s24, 1", "s_cmp_ge_u32 s24, %6", f"s_cbranch_scc0 .Lvx_cont{k}_%=", "s_barrier",
-                  "s_branch .Lvx_end%=", "s_nop 0", ".p2align 3", f".Lvx_cont{k}_%=:"]
-            continue
-        L += ["s_barrier", "s_add_u32 s24, s24, 1"]
-        if mode == "burst2":  # next block's slot: (b + 2) % 3
-            L += [f"s_add_u32 s25, s25, {SLOT_BYTES}", f"s_cmp_eq_u32 s25, {3 * SLOT_BYTES}",
-                  "s_cselect_b32 s25, 0, s25", "s_nop 0"]
-        L += ["s_cmp_ge_u32 s24, %6", "s_cbranch_scc1 .Lvx_end%=", ".p2align 3"]
+        L += ["s_barrier", "s_add_u32 s24, s24, 1", "s_cmp_ge_u32 s24, %6", "s_cbranch_scc1 .Lvx_end%=",
+              ".p2align 3"]
     L += ["s_branch .Lvx_loop%=", ".Lvx_end%=:", "s_waitcnt lgkmcnt(0)"]
     L += [f"v_mov_b32_e64 %{i}, v{H0 + i}" for i in range(5)]
     return "\n".join(L)
 
 
-FLAG_V, CONS_V = "v88", "v89"  # flags mode: last read of the producer's count; the count we publish
-SPIN_LIMIT = 1 << 22           # polls (s_sleep 1 each, ~64 cycles) before a wait gives up: ~0.1-0.3 s
-
-
-def _spin(label: str, need: str) -> list:
-    """Wait until the producer's published count (LDS dword at %9) is >= the
-    SGPR `need`.  FLAG_V already holds a recent read of it (lgkmcnt settled), so
-    the fast path is v_readfirstlane + compare + branch.  The slow path polls with
-    s_sleep; after SPIN_LIMIT polls it gives up and sets s29 = 1 (the block is then
-    hashed from a stale slot; the exit stores s29 at %9 + 8 for the caller to
-    report as a failed launch)."""
-    return [f".Lvx_{label}%=:", f"v_readfirstlane_b32 s26, {FLAG_V}", f"s_cmp_ge_u32 s26, {need}",
-            f"s_cbranch_scc1 .Lvx_{label}ok%=", "s_add_u32 s28, s28, 1", f"s_cmp_ge_u32 s28, {SPIN_LIMIT}",
-            f"s_cbranch_scc1 .Lvx_{label}bail%=", "s_sleep 1", f"ds_read_b32 {FLAG_V}, %9",
-            "s_waitcnt lgkmcnt(0)", f"s_branch .Lvx_{label}%=", f".Lvx_{label}bail%=:", "s_mov_b32 s29, 1",
-            f".Lvx_{label}ok%=:"]
-
-
-def consumer_flags_asm(select: bool) -> str:
-    """The consumer with an LDS flag handshake instead of s_barrier (3 slots,
-    burst reads).  %9 = LDS byte address of two dwords {prod, cons}: the
-    producer stores prod = j + 1 after block j's slot is written; the consumer
-    stores cons = b + 2 once block b + 1's slot is in registers (end of block b),
-    and the producer writes block j only when cons >= j - 2.  At the top of
-    block b the consumer needs prod >= b + 2 (block b + 1 published) unless b is
-    its last block; the count it tests was read at the top of block b - 1, so
-    in steady state (producer ahead) the wait is one readfirstlane + compare.
-    Other operands as consumer_asm.  On exit the dword at %9 + 8 is 1 if a wait
-    gave up (never in a correct pairing; a bounded wait keeps a protocol bug
-    from hanging the GPU), else 0."""
-    L = [f"v_mov_b32_e64 v{H0 + i}, %{i}" for i in range(5)]
-    L += ["s_mov_b32 s20, 0x5a827999", "s_mov_b32 s21, 0x6ed9eba1", "s_mov_b32 s22, 0x8f1bbcdc",
-          "s_mov_b32 s23, 0xca62c1d6", "s_mov_b32 s24, 0", "s_mov_b32 s28, 0", "s_mov_b32 s29, 0",
-          "s_mov_b32 s27, 1", "s_cmp_eq_u32 %6, 0", "s_cbranch_scc1 .Lvx_end%=",
-          f"ds_read_b32 {FLAG_V}, %9", "s_waitcnt lgkmcnt(0)"]
-    L += _spin("w0", "s27")
-    L += [_read(WA, q, 0) for q in range(20)]
-    L += ["s_waitcnt lgkmcnt(0)", f"v_mov_b32_e64 {CONS_V}, 1", f"ds_write_b32 %9, {CONS_V} offset:4",
-          ".p2align 5", ".Lvx_loop%=:"]
-    for k in range(6):
-        cur = WA if k % 2 == 0 else WB
-        nxt = WB if cur == WA else WA
-        # s27 = b + 2: the count block b + 1 needs, and what we publish at the end
-        L += ["s_add_u32 s27, s24, 2", "s_cmp_gt_u32 s27, %6", f"s_cbranch_scc1 .Lvx_w{k + 1}ok%="]
-        L += _spin(f"w{k + 1}", "s27")
-        L += [f"ds_read_b32 {FLAG_V}, %9", "s_nop 0", ".p2align 3"]
-        body = _block(consumer_regs(cur), "burst", (k + 1) % 3, nxt)
-        if select:
-            L += ["s_cmp_lt_u32 s24, %7", f"s_cbranch_scc0 .Lvx_sel{k}_%=", ".p2align 3"]
-            L += body
-            L += [f"s_branch .Lvx_done{k}_%=", "s_nop 0", ".p2align 3", f".Lvx_sel{k}_%=:"]
-            L += [f"v_mov_b32_e64 v{SAVE0 + i}, v{H0 + i}" for i in range(5)]
-            L += body
-            L += ["v_cmp_lt_u32_e64 vcc, s24, %8"]
-            L += [f"v_cndmask_b32_e64 v{H0 + i}, v{SAVE0 + i}, v{H0 + i}, vcc" for i in range(5)]
-            L += [".p2align 3", f".Lvx_done{k}_%=:"]
-        else:
-            L += body
-        # body ends with lgkmcnt(0): block b + 1's words (and the count read) are in registers
-        L += [f"v_mov_b32_e64 {CONS_V}, s27", f"ds_write_b32 %9, {CONS_V} offset:4",
-              "s_add_u32 s24, s24, 1", "s_cmp_ge_u32 s24, %6", "s_cbranch_scc1 .Lvx_end%=", ".p2align 3"]
-    L += ["s_branch .Lvx_loop%=", ".Lvx_end%=:", f"v_mov_b32_e64 {CONS_V}, s29",
-          f"ds_write_b32 %9, {CONS_V} offset:8", "s_waitcnt lgkmcnt(0)"]
-    L += [f"v_mov_b32_e64 %{i}, v{H0 + i}" for i in range(5)]
-    return "\n".join(L)
-
-
-def consumer_clobbers(select: bool, mode: str = "burst", flags: bool = False):
-    v = [f"v{i}" for i in range(H0, SAVE0 + 5 if select else SAVE0)] + ([ADDR] if mode == "burst2" else [])
-    v += [FLAG_V, CONS_V] if flags else []
-    v += [f"v{i}" for i in range(WA, (WA if mode == "refill" else WB) + 80)]
+def consumer_clobbers(select: bool):
+    v = [f"v{i}" for i in range(H0, SAVE0 + 5 if select else SAVE0)]
+    v += [f"v{i}" for i in range(WA, WB + 80)]
     # s_cmp_* / s_add_u32 in the loop control write SCC: name it, so the compiler
     # never keeps a compare live in SCC across the asm body
-    return v + ["s20", "s21", "s22", "s23", "s24", "s25", "vcc", "scc"] + (["s26", "s27", "s28", "s29"] if flags
-                                                                           else [])
+    return v + ["s20", "s21", "s22", "s23", "s24", "s25", "vcc", "scc"]
 
 
-def write_consumerf_header(path: str) -> None:
-    with open(path, "w") as f:
-        f.write("// GENERATED by tools/gen_sha1_rounds.py --consumerf; do not edit.\n"
-                "// The split kernels' consumer loop with an LDS flag handshake instead of\n"
-                "// s_barrier (3 slots, burst reads; consumer_flags_asm).\n#pragma once\n\n")
-        for name, sel in (("VX_CONSUMERF_ASM", False), ("VX_CONSUMERF_SELECT_ASM", True)):
-            f.write(f"#define {name} \\\n")
-            for line in consumer_flags_asm(sel).splitlines():
-                f.write(f'    "{line}\\n" \\\n')
-            f.write('    ""\n')
-            f.write(f"#define {name}_CLOBBERS " + ", ".join(f'"{r}"' for r in consumer_clobbers(sel, flags=True))
-                    + "\n\n")
-
-
-def write_consumer_header(path: str, mode: str, slots: int = 3) -> None:
+def write_consumer_header(path: str, mode: str = "burst") -> None:
     with open(path, "w") as f:
         f.write("// GENERATED by tools/gen_sha1_rounds.py --consumer; do not edit.\n"
                 "// The split kernels' consumer loop (ring of 3 LDS slots) as one asm body:\n"
                 "// fixed issue order and registers for the 80 SHA-1 rounds (DESIGN.md §3.2).\n"
                 "// Checked by tests/test_rounds_gen.py (stream simulated against FIPS 180-4,\n"
                 f"// header up to date).  Ring reads: {mode}.\n#pragma once\n\n")
-        names = (("VX_CONSUMER_ASM", False), ("VX_CONSUMER_SELECT_ASM", True)) if slots == 3 else \
-            (("VX_CONSUMER6_ASM", False), ("VX_CONSUMER6_SELECT_ASM", True))
-        for name, sel in names:
+        for name, sel in (("VX_CONSUMER_ASM", False), ("VX_CONSUMER_SELECT_ASM", True)):
             f.write(f"#define {name} \\\n")
-            for line in consumer_asm(sel, mode, slots).splitlines():
+            for line in consumer_asm(sel).splitlines():
                 f.write(f'    "{line}\\n" \\\n')
             f.write('    ""\n')
-            f.write(f"#define {name}_CLOBBERS " + ", ".join(f'"{r}"' for r in consumer_clobbers(sel, mode)) + "\n\n")
+            f.write(f"#define {name}_CLOBBERS " + ", ".join(f'"{r}"' for r in consumer_clobbers(sel)) + "\n\n")
 
 
 # ---- simulation (the --check) -------------------------------------------
@@ -424,58 +280,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--emit", action="store_true", help="print the asm body (default registers)")
-    ap.add_argument("--header", help="write a C header with the fixed-register block (probe use)")
     ap.add_argument("--consumer", help="write the split kernels' consumer asm header")
-    ap.add_argument("--consumer6", help="write the 6-slot, barrier-per-pair consumer header (probe only: "
-                                           "no faster in the kernels, DESIGN.md §3.2.1)")
-    ap.add_argument("--consumerf", help="write the flag-handshake consumer header (consumer_flags_asm)")
-    ap.add_argument("--consumer-placements", help="probe only: no-barrier consumers with the ring reads placed "
-                                                  "none / split2 / split4 / spread4 / late")
-    ap.add_argument("--consumer-nobarrier", help="probe only: the 3-slot consumer with every s_barrier replaced "
-                                                 "by s_nop 0 (what the barrier costs; no synchronisation)")
-    ap.add_argument("--mode", default="burst", choices=["refill", "burst", "burst2", "spread", "split2", "split4", "late"],
-                    help="ring-read placement (burst: the kernel's; A/B in DESIGN.md §3.2)")
     a = ap.parse_args()
     if a.check:
         check()
-    R = default_regs()
-    ins, final = rounds(R)
     if a.emit:
-        print(emit(ins, final, R.h))
+        R = default_regs()
+        print(emit(*rounds(R), R.h))
     if a.consumer:
-        write_consumer_header(a.consumer, a.mode)
-    if a.consumer6:
-        write_consumer_header(a.consumer6, a.mode, slots=6)
-    if a.consumerf:
-        write_consumerf_header(a.consumerf)
-    if a.consumer_placements:
-        with open(a.consumer_placements, "w") as f:
-            f.write("// GENERATED by tools/gen_sha1_rounds.py --consumer-placements; do not edit.\n"
-                    "// Probe only: the consumer (no barriers) with the ring reads placed per mode.\n#pragma once\n\n")
-            for m in ("none", "split2", "split4", "spread4", "late"):
-                f.write(f"#define VX_CONSUMERNB_{m.upper()}_ASM \\\n")
-                for line in consumer_asm(False, m).replace("s_barrier", "s_nop 0").splitlines():
-                    f.write(f'    "{line}\\n" \\\n')
-                f.write('    ""\n')
-    if a.consumer_nobarrier:
-        with open(a.consumer_nobarrier, "w") as f:
-            f.write("// GENERATED by tools/gen_sha1_rounds.py --consumer-nobarrier; do not edit.\n"
-                    "// Probe only: the consumer with s_barrier -> s_nop 0 (no synchronisation).\n#pragma once\n\n")
-            f.write("#define VX_CONSUMERNB_ASM \\\n")
-            for line in consumer_asm(False, "burst").replace("s_barrier", "s_nop 0").splitlines():
-                f.write(f'    "{line}\\n" \\\n')
-            f.write('    ""\n')
-    if a.header:
-        body = emit(ins, final, R.h)
-        regs = sorted({r for r in R.h + R.w + R.a + R.c + R.x + R.f + [R.r]}, key=lambda r: int(r[1:]))
-        with open(a.header, "w") as f:
-            f.write("// generated by tools/gen_sha1_rounds.py --header: one SHA-1 block (80 rounds +\n"
-                    "// feed-forward) on fixed registers: state v60-v64, words v100-v179, K in s20-s23.\n")
-            f.write("#define VX_ROUNDS_FIXED \\\n")
-            for line in body.splitlines():
-                f.write(f'    "{line}\\n" \\\n')
-            f.write('    ""\n')
-            f.write("#define VX_ROUNDS_FIXED_CLOBBERS " + ", ".join(f'"{r}"' for r in regs) + "\n")
+        write_consumer_header(a.consumer)
 
 
 if __name__ == "__main__":
