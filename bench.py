@@ -496,6 +496,36 @@ def drop_cache(path: str) -> float | None:
     return resident_fraction(path)
 
 
+def disk_direct_rate(path: str, total: int, threads: int, bs: int = 1 << 20) -> float | None:
+    """The disk's own O_DIRECT read rate over the (evicted) file: `threads`
+    threads, one bs-byte read in flight each, no copy and no hash (the cold
+    leg's reference for what the disk gives; tools/disk_qd_probe.py).  None
+    where the filesystem refuses O_DIRECT."""
+    import mmap
+    from concurrent.futures import ThreadPoolExecutor
+
+    try:
+        fd = os.open(path, os.O_RDONLY | os.O_DIRECT)
+    except OSError:
+        return None
+    n = (total + bs - 1) // bs
+
+    def work(t: int) -> int:
+        buf = mmap.mmap(-1, bs)  # page-aligned, as O_DIRECT needs
+        return sum(os.preadv(fd, [buf], i * bs) for i in range(t, n, threads))
+
+    try:
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(threads) as ex:
+            got = sum(ex.map(work, range(threads)))
+        el = time.perf_counter() - t0
+    except OSError:
+        return None
+    finally:
+        os.close(fd)
+    return got / el / GiB if got == total else None
+
+
 def reverify_dir() -> str:
     """Where the config-5 file goes: the first candidate on a disk-backed
     filesystem (a 'cold' read from tmpfs would still be a memory copy)."""
@@ -604,7 +634,9 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
             just wrote or read);
       cold  every call preceded by fsync + POSIX_FADV_DONTNEED, so the reads
             go to the disk (vortex starting up on a torrent whose data is not
-            cached); the resident fraction before each call is recorded.
+            cached); the resident fraction before each call is recorded, and
+            the disk alone (disk_direct_rate: O_DIRECT reads of the evicted
+            file by as many threads, no copy, no hash) alternates with both.
     Each GPU call's time budget (vx_tuning_last_verify: reader busy time and
     rate, GPU-timed copy busy fraction) goes into the record."""
     import oracle
@@ -637,7 +669,7 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
             assert all(got) and bad == 0
             pool.reset_stats()
             for leg in ("warm", "cold"):
-                gpu_t, cpu_t, traces, resident = [], [], [], []
+                gpu_t, cpu_t, traces, resident, disk = [], [], [], [], []
                 for _ in range(reps if leg == "warm" else cold_reps):
                     if leg == "cold":
                         resident.append(drop_cache(path))
@@ -654,7 +686,10 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
                     cpu = oracle.pool_verify_files([path], [total], pl, exp, threads=threads)
                     cpu_t.append(time.perf_counter() - t0)
                     assert all(cpu)
-                legs[leg] = (gpu_t, cpu_t, traces, resident)
+                    if leg == "cold":  # the disk alone, same file, same readers, evicted again
+                        drop_cache(path)
+                        disk.append(disk_direct_rate(path, total, threads))
+                legs[leg] = (gpu_t, cpu_t, traces, resident, disk)
             st = pool.stats()
             # the split (vx_plan_verify_split with the pool's per-thread rate just measured), warm
             for _ in range(2):
@@ -695,8 +730,10 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
             os.unlink(path)
 
     def record(leg):
-        gpu_t, cpu_t, traces, resident = legs[leg]
+        gpu_t, cpu_t, traces, resident, disk = legs[leg]
         g, c = sorted(gpu_t)[len(gpu_t) // 2], sorted(cpu_t)[len(cpu_t) // 2]
+        dk = sorted(x for x in disk if x)
+        dmed = dk[len(dk) // 2] if dk else None
         # the median call's copy-engine gaps by cause (its full timeline stays in gpu_traces)
         med_trace = traces[sorted(range(len(gpu_t)), key=lambda i: gpu_t[i])[len(gpu_t) // 2]]
         # what bound this box's calls: the H2D copies busy nearly all
@@ -716,7 +753,9 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
         for t in traces:  # one full timeline (the median call's) is enough for the record
             if t is not med_trace:
                 t.pop("timeline", None)
-        return {"value": round(total / g / GiB, 2), "unit": "GiB/s", "bound": bound,
+        if leg == "cold" and dmed:
+            bound = (bound or "") + f"; the disk alone (O_DIRECT, {threads} threads, 1 MiB) {dmed:.1f} GiB/s"
+        out = {"value": round(total / g / GiB, 2), "unit": "GiB/s", "bound": bound,
                 "copy_gaps": med_trace.get("copy_gaps"),
                 "gpu_s_runs": [round(t, 4) for t in gpu_t],
                 "cpu_pool": {"value": round(total / c / GiB, 2), "unit": "GiB/s", "cores": threads, "kind": "port",
@@ -724,6 +763,11 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
                 "gpu_over_cpu": round(c / g, 3),
                 "resident_before_calls": [None if r is None else round(r, 4) for r in resident],
                 "gpu_traces": traces}
+        if leg == "cold":
+            out["disk_direct"] = {"value": None if dmed is None else round(dmed, 2), "unit": "GiB/s",
+                                  "runs": [None if x is None else round(x, 2) for x in disk],
+                                  "gpu_frac_of_disk": None if not dmed else round(total / g / GiB / dmed, 3)}
+        return out
 
     warm, cold = record("warm"), record("cold")
     best = max(split["configs"], key=lambda c: c["value"])

@@ -338,6 +338,23 @@ def test_node_cpus_honours_cgroup_quota(tmp_path):
     assert bench.node_cpus(str(tmp_path / "absent")) == aff
 
 
+def test_disk_direct_rate_reads_the_whole_file(tmp_path):
+    """The cold leg's disk reference (bench.disk_direct_rate): O_DIRECT reads
+    of the evicted file in 1 MiB blocks, a ragged tail included, counted only
+    when every byte came back; None where the filesystem refuses O_DIRECT."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    size = (3 << 20) + 4097
+    p = tmp_path / "f.bin"
+    p.write_bytes(os.urandom(size))
+    bench.drop_cache(str(p))
+    r = bench.disk_direct_rate(str(p), size, 3)
+    assert r is None or r > 0
+    if r is not None:  # a wrong total is never reported as a rate
+        assert bench.disk_direct_rate(str(p), size + 1, 3) is None
+
+
 def test_roofline_scalars_for_the_record():
     """The driver keeps only the scalar fields of `roofline`: the clock the
     run held and the kernel's fraction of its binding (VALU-issue) roof must
