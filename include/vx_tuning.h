@@ -52,6 +52,10 @@ void vx_tuning_fail_launch_after(struct vx_ctx* ctx, int64_t k);
  * both on the slot's stream behind a host wait for the previous round's copy
  * (round 4's form). */
 void vx_tuning_verify_copy_stream(struct vx_ctx* ctx, int mode);
+/* A/B of the pinned stages' memory: on = 1 allocates them as
+ * 2 MiB-aligned transparent-huge-page mappings registered with hipHostRegister,
+ * 0 with hipHostMalloc.  Idle stages are freed and reallocated on next use. */
+void vx_tuning_stage_huge(struct vx_ctx* ctx, int on);
 /* The kernel vx_sha1_device_ragged_hint runs for a batch of n pieces whose
  * longest is max_len bytes, total_len bytes in all: 1 = lane, 2 = split,
  * 5 = split with one pair per CU (host-only). */

@@ -7,12 +7,15 @@
 // the pipeline's copy chain does).  Tells whether the readers bind by
 // themselves or only inside the full pipeline.
 //
-// usage: readers_probe <file> <piece_len> [threads=16] [chunk=262144] [ahead=2] [stages=4] [dio=1] [dma=0] [reps=3] [evict=0]
+// usage: readers_probe <file> <piece_len> [threads=16] [chunk=262144] [ahead=2] [stages=4] [dio=1] [dma=0] [reps=3] [evict=0] [mem=0]
 //   evict=1: drop the file's pages (fsync + POSIX_FADV_DONTNEED) before every rep (a cold re-verify)
+//   mem: the stages' memory, 0 hipHostMalloc (the engine's), 1 plain mmap (not pinned), 2 mmap + hipHostRegister,
+//        3 / 4 as 1 / 2 with MADV_HUGEPAGE (2 MiB pages where THP allows)
 // Prints one JSON line: best GiB/s over reps, the readers' own rate (bytes /
 // summed pread time) and, with dma, the copy rate.
 #include <fcntl.h>
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -37,6 +40,7 @@ int main(int argc, char** argv) {
     const bool dma = argc > 8 ? std::atoi(argv[8]) != 0 : false;
     const int reps = argc > 9 ? std::atoi(argv[9]) : 3;
     const bool evict = argc > 10 ? std::atoi(argv[10]) != 0 : false;
+    const int mem = argc > 11 ? std::atoi(argv[11]) : 0;
     const int fd = open(path, O_RDONLY | O_CLOEXEC);
     struct stat st;
     if (fd < 0 || fstat(fd, &st) != 0) return 3;
@@ -46,8 +50,22 @@ int main(int argc, char** argv) {
     const uint64_t pitch = (C + 4095) / 4096 * 4096;
     const uint64_t stage_bytes = n * pitch;
     std::vector<uint8_t*> stage(nst, nullptr);
-    for (auto& s : stage)
-        if (hipHostMalloc(&s, stage_bytes, hipHostMallocDefault) != hipSuccess) return 4;
+    for (auto& s : stage) {
+        if (mem == 0) {
+            if (hipHostMalloc(&s, stage_bytes, hipHostMallocDefault) != hipSuccess) return 4;
+            continue;
+        }
+        const bool huge = mem >= 3;
+        void* p = mmap(nullptr, stage_bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS | (huge ? 0 : MAP_POPULATE),
+                       -1, 0);
+        if (p == MAP_FAILED) return 4;
+        s = static_cast<uint8_t*>(p);
+        if (huge) {
+            (void)madvise(s, stage_bytes, MADV_HUGEPAGE);
+            for (uint64_t o = 0; o < stage_bytes; o += 4096) s[o] = 0;
+        }
+        if ((mem == 2 || mem == 4) && hipHostRegister(s, stage_bytes, hipHostRegisterDefault) != hipSuccess) return 4;
+    }
     uint8_t* dev = nullptr;
     hipStream_t ds = nullptr;
     if (dma && (hipMalloc(&dev, stage_bytes) != hipSuccess || hipStreamCreate(&ds) != hipSuccess)) return 5;
@@ -114,10 +132,18 @@ int main(int argc, char** argv) {
         }
     }
     std::printf("{\"threads\": %d, \"chunk\": %llu, \"ahead\": %zu, \"stages\": %d, \"dio\": %d, \"dma\": %d, "
-                "\"evict\": %d, \"GiBps\": %.2f, \"reader_own_GiBps_per_thread\": %.2f, \"copy_GiBps\": %.2f}\n",
-                threads, (unsigned long long)C, ahead, nst, (int)use_dio, (int)dma, (int)evict, best, best_own,
+                "\"evict\": %d, \"mem\": %d, \"GiBps\": %.2f, \"reader_own_GiBps_per_thread\": %.2f, "
+                "\"copy_GiBps\": %.2f}\n",
+                threads, (unsigned long long)C, ahead, nst, (int)use_dio, (int)dma, (int)evict, mem, best, best_own,
                 best_copy);
-    for (auto s : stage) (void)hipHostFree(s);
+    for (auto s : stage) {
+        if (mem == 0) {
+            (void)hipHostFree(s);
+            continue;
+        }
+        if (mem == 2 || mem == 4) (void)hipHostUnregister(s);
+        munmap(s, stage_bytes);
+    }
     if (dev) (void)hipFree(dev);
     close(fd);
     return 0;

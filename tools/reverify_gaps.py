@@ -4,10 +4,10 @@ vx_verify_files over the linux-mint-geometry file for several context shapes,
 alternating, each call's round timeline (vx_last_verify_rounds) reduced by
 bench.copy_gaps to gaps by cause and by slot.  Prints one JSON line.
 
-Shapes: "<slots>" (the engine's default: data copies on the context's copy
+Shapes: "<slots>[s][h]"; "<slots>" (the engine's default: data copies on the context's copy
 stream, lane tables on the slot streams) or "<slots>s" (each copy on its
 slot's stream, round 4's form): vx_tuning_verify_copy_stream(ctx, 1 / 0),
-test build.  (Round 5 also measured the tables on the copy stream, and a
+test build; "h": pinned stages on huge pages (vx_tuning_stage_huge).  (Round 5 also measured the tables on the copy stream, and a
 normal-priority copy stream: EXPERIMENTS.md §6.3.)
 
 With --split "io:pool:gpu_frac,...": instead, the split of DESIGN.md §6.6
@@ -17,6 +17,7 @@ on the GPU, configs alternating call by call.
 
 usage: python tools/reverify_gaps.py [--reps 5] [--slots 4,4s,6,6s] [--scale 1.0]
        python tools/reverify_gaps.py --split 8:16:0.55,8:8:0.6,4:12:0.55 [--reps 9]
+       python tools/reverify_gaps.py --cold 0,0h,1048576 [--reps 5]
 """
 import argparse
 import json
@@ -35,6 +36,8 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--split", default="")
     ap.add_argument("--geometry", default="", help="N:MiB = N pieces of MiB each instead of linux-mint's")
+    ap.add_argument("--cold", default="", help="cold A/B instead: verify_cold_chunk values, e.g. 0,1048576,0h (h: "
+                                               "huge-page stages); each evicted call followed by the disk alone")
     a = ap.parse_args()
     import bench
     import oracle
@@ -61,7 +64,9 @@ def main():
         else:
             total, n, last = bench.write_linuxmint_file(path, a.scale)
         exp = oracle.pool_digest_synth(0x5EED0005, 0, n, pl, last_index=n - 1, last_len=last, threads=threads)
-        if a.split:
+        if a.cold:
+            out["cold"] = cold_ab(a, path, total, n, pl, exp, threads)
+        elif a.split:
             out["split"] = split_sweep(a, path, total, n, pl, exp)
         else:
             slots_ab(a, out, path, total, n, pl, exp, threads)
@@ -77,9 +82,10 @@ def slots_ab(a, out, path, total, n, pl, exp, threads):
 
     shapes = a.slots.split(",")
     pools = {}
-    for s in shapes:
-        pools[s] = HashPool(pl, slots=int(s.rstrip("s")), slot_bytes=512 << 20, batch_pieces=4096, hooks=True)
-        pools[s].lib.vx_tuning_verify_copy_stream(pools[s]._h, 0 if s.endswith("s") else 1)
+    for s in shapes:  # "<slots>[s][h]": s = slot-stream copies, h = huge-page stages
+        pools[s] = HashPool(pl, slots=int(s.rstrip("sh")), slot_bytes=512 << 20, batch_pieces=4096, hooks=True)
+        pools[s].lib.vx_tuning_verify_copy_stream(pools[s]._h, 0 if s.rstrip("h").endswith("s") else 1)
+        pools[s].lib.vx_tuning_stage_huge(pools[s]._h, int(s.endswith("h")))
     runs = {s: [] for s in shapes}
     for s, pool in pools.items():  # warm every context (stages, rows, page cache)
         got, bad = pool.verify_files([path], [total], pl, exp, io_threads=threads)
@@ -94,7 +100,7 @@ def slots_ab(a, out, path, total, n, pl, exp, threads):
             tr = pool.last_verify()
             g = bench.copy_gaps(rounds)
             by_slot = {}
-            ns = int(s.rstrip("s"))
+            ns = int(s.rstrip("sh"))
             for k in range(1, len(rounds)):
                 gap = rounds[k]["copy_start_ms"] - rounds[k - 1]["copy_end_ms"]
                 by_slot[k % ns] = round(by_slot.get(k % ns, 0.0) + max(0.0, gap), 3)
@@ -112,6 +118,45 @@ def slots_ab(a, out, path, total, n, pl, exp, threads):
         out["shapes"][f"slots{s}"] = {"median_GiBps": r[len(r) // 2]["GiBps"], "runs": runs[s]}
     for p in pools.values():
         p.close()
+
+
+def cold_ab(a, path, total, n, pl, exp, threads):
+    """Evicted re-verify calls per verify_cold_chunk value, alternating, each
+    followed by the disk's own O_DIRECT rate over the same evicted file."""
+    import bench
+    from vortex_amd.hash_pool import HashPool
+
+    # "<verify_cold_chunk>[h][@<slot MiB>]": h = huge-page stages (vx_tuning_stage_huge)
+    chunks = a.cold.split(",")
+    pools = {}
+    for ch in chunks:
+        spec, _, mib = ch.partition("@")
+        pools[ch] = HashPool(pl, slots=4, slot_bytes=int(mib or 512) << 20, batch_pieces=4096,
+                             verify_cold_chunk=int(spec.rstrip("h")), hooks=True)
+        pools[ch].lib.vx_tuning_stage_huge(pools[ch]._h, int(spec.endswith("h")))
+    res = {ch: [] for ch in chunks}
+    for ch, pool in pools.items():
+        pool.verify_files([path], [total], pl, exp, io_threads=threads)
+    for _ in range(a.reps):
+        for ch, pool in pools.items():
+            bench.drop_cache(path)
+            t0 = time.perf_counter()
+            got, bad = pool.verify_files([path], [total], pl, exp, io_threads=threads)
+            el = time.perf_counter() - t0
+            assert all(got) and bad == 0
+            tr = pool.last_verify()
+            bench.drop_cache(path)
+            disk = bench.disk_direct_rate(path, total, threads)
+            res[ch].append({"GiBps": round(total / el / (1 << 30), 2), "disk_GiBps": disk and round(disk, 2),
+                            "chunk_bytes": tr["chunk_bytes"], "copy_busy_frac": round(tr["copy_busy_frac"], 3),
+                            "read_GiBps": round(tr["read_GiBps"], 2)})
+    for p in pools.values():
+        p.close()
+    out = {}
+    for ch, runs in res.items():
+        r = sorted(x["GiBps"] for x in runs)
+        out[ch] = {"median_GiBps": r[len(r) // 2], "runs": runs}
+    return out
 
 
 def split_sweep(a, path, total, n, pl, exp):

@@ -26,6 +26,7 @@
 
 #include <fcntl.h>
 #include <sched.h>
+#include <sys/mman.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -97,6 +98,7 @@ struct Slot {
     uint32_t cap = 0;  // pieces
     uint8_t* d_arena = nullptr;
     uint8_t* h_stage = nullptr;
+    uint64_t stage_map = 0;  // > 0: h_stage is a registered mmap of this many bytes (alloc_stage)
     // pinned metadata block: offsets | lens | expected | digests | matched
     uint8_t* h_meta = nullptr;
     uint8_t* d_meta = nullptr;
@@ -215,6 +217,9 @@ struct vx_ctx {
     // copies for A/B.
     hipStream_t copy_stream = nullptr;
     int verify_copy_stream = 1;
+    // How pinned stages are allocated (alloc_stage): 1 = 2 MiB-aligned mmap
+    // with transparent huge pages, then hipHostRegister; 0 = hipHostMalloc.
+    int stage_huge = 0;
     hipEvent_t anchor_ev = nullptr;            // maps the rounds' GPU times onto the host clock
     uint64_t verify_t0_ns = 0;                 // the running re-verify call's start (steady clock)
 };
@@ -251,6 +256,46 @@ bool is_registered(const vx_ctx* c, const void* p, size_t len, const uint8_t** d
     return true;
 }
 
+// Pinned stage memory.  huge: an anonymous mapping aligned to 2 MiB with
+// MADV_HUGEPAGE, faulted in, then registered (hipHostRegister), so the
+// readers' O_DIRECT reads and the H2D copies touch 512x fewer page-table and
+// IOMMU entries than with hipHostMalloc's 4 KiB pages.
+uint8_t* alloc_stage(uint64_t bytes, bool huge, uint64_t* mapped) {
+    *mapped = 0;
+    if (!huge) {
+        uint8_t* p = nullptr;
+        return hipHostMalloc(&p, bytes, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+    }
+    constexpr uint64_t kHuge = 2ull << 20;
+    const uint64_t len = (bytes + kHuge - 1) / kHuge * kHuge;
+    void* raw = mmap(nullptr, len + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (raw == MAP_FAILED) return nullptr;
+    const uintptr_t r = reinterpret_cast<uintptr_t>(raw), a = (r + kHuge - 1) / kHuge * kHuge;
+    if (a > r) munmap(raw, a - r);  // trim to the aligned [a, a + len)
+    if (r + len + kHuge > a + len) munmap(reinterpret_cast<void*>(a + len), r + len + kHuge - (a + len));
+    uint8_t* p = reinterpret_cast<uint8_t*>(a);
+    (void)madvise(p, len, MADV_HUGEPAGE);  // a hint: 4 KiB pages where THP is off
+    for (uint64_t o = 0; o < len; o += 4096) p[o] = 0;
+    if (hipHostRegister(p, len, hipHostRegisterDefault) != hipSuccess) {
+        munmap(p, len);
+        return nullptr;
+    }
+    *mapped = len;
+    return p;
+}
+
+void free_stage(Slot& s) {
+    if (!s.h_stage) return;
+    if (s.stage_map) {
+        (void)hipHostUnregister(s.h_stage);
+        munmap(s.h_stage, s.stage_map);
+    } else {
+        (void)hipHostFree(s.h_stage);
+    }
+    s.h_stage = nullptr;
+    s.stage_map = 0;
+}
+
 int free_slot_mem(Slot& s) {
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (s.done) (void)hipEventDestroy(s.done);
@@ -258,7 +303,7 @@ int free_slot_mem(Slot& s) {
     if (s.stream) (void)hipStreamDestroy(s.stream);
     if (s.d_arena) (void)hipFree(s.d_arena);
     if (s.d_meta) (void)hipFree(s.d_meta);
-    if (s.h_stage) (void)hipHostFree(s.h_stage);
+    free_stage(s);
     if (s.h_meta) (void)hipHostFree(s.h_meta);
     s = Slot{};
     return 0;
@@ -310,12 +355,10 @@ int alloc_slot(Slot& s, uint64_t arena, uint32_t cap) {
 }
 
 // Pinned stage of slot s (unregistered pieces, file reads), allocated on first use.
-int ensure_stage(Slot& s) {
+int ensure_stage(const vx_ctx* c, Slot& s) {
     if (s.h_stage) return 0;
-    if (hipHostMalloc(&s.h_stage, s.arena_cap, hipHostMallocDefault) != hipSuccess) {
-        s.h_stage = nullptr;
-        return fail(VX_ENOMEM, "pinned stage allocation failed");
-    }
+    s.h_stage = alloc_stage(s.arena_cap, c->stage_huge != 0, &s.stage_map);
+    if (!s.h_stage) return fail(VX_ENOMEM, "pinned stage allocation failed");
     return 0;
 }
 
@@ -698,7 +741,7 @@ int submit_impl(vx_ctx* c, uint64_t tag, const uint8_t* data, uint32_t len, cons
             else
                 s->druns.push_back(DirectRun{data, off, off + len});
         } else {
-            if (int rc = ensure_stage(*s)) return rc;
+            if (int rc = ensure_stage(c, *s)) return rc;
             c->stats.staged_bytes += len;
             if (c->bulk) {  // a host batch: copied in parallel at launch (stage_copies)
                 s->staged.push_back(StageCopy{data, off, len});
@@ -1126,7 +1169,7 @@ int verify_whole(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl,
             if (rc || si < 0) break;
             Slot& s = c->slots[si];
             reset_fill(s);
-            if ((rc = ensure_stage(s))) break;
+            if ((rc = ensure_stage(c, s))) break;
             s.state = Slot::FILLING;  // reserved until launched
             s.t_open = std::chrono::steady_clock::now();
             uint64_t cap = filled < ramp ? std::max<uint64_t>(1, cap_full >> (ramp - filled)) : cap_full;
@@ -1509,7 +1552,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
         if (rc || si < 0) return false;
         Slot& s = c->slots[si];
         reset_fill(s);
-        if ((rc = ensure_stage(s))) return false;
+        if ((rc = ensure_stage(c, s))) return false;
         // lanes 4 KiB apart: every stage destination can take an O_DIRECT read
         const uint64_t pitch = align_up(r.len, vx_files::DirectIo::kBlock);
         auto& it = items[si];
@@ -2262,6 +2305,12 @@ void vx_tuning_fail_launch_after(vx_ctx* c, int64_t k) {
 }
 void vx_tuning_verify_copy_stream(vx_ctx* c, int mode) {
     if (c) c->verify_copy_stream = mode ? 1 : 0;
+}
+void vx_tuning_stage_huge(vx_ctx* c, int on) {
+    if (!c) return;
+    c->stage_huge = on ? 1 : 0;
+    for (auto& s : c->slots)  // reallocated on next use (every slot is idle between calls)
+        if (s.state == Slot::FREE) free_stage(s);
 }
 #endif
 size_t vx_tuning_chunk_schedule(uint64_t L, uint64_t C, int head, int tail, uint64_t* out, size_t max) {
