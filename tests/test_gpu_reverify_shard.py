@@ -94,6 +94,33 @@ def test_split_verify_with_the_pool(built, gpu, tmp_path, pl):
             assert r["ok"] is False  # the damaged pieces mismatch on whichever side holds them
 
 
+@pytest.mark.parametrize("pl", [256 * 1024, 1 << 20])
+def test_stage_memory_kinds(built, gpu, tmp_path, pl):
+    """The pinned stages the readers fill: huge-page mappings registered with
+    hipHostRegister (the default) and hipHostMalloc (vx_tuning_stage_huge 0,
+    test build), switched back and forth on one context (idle stages are freed
+    and reallocated); every verdict equals the pool restatement's, warm and
+    with the files evicted (direct reads into the stages)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from vortex_amd.hash_pool import HashPool
+
+    sizes = [3, 4 * pl + 17, 2 * pl, 0, 3 * pl - 5, pl + 1, 64, 2 * pl + pl // 2]
+    paths, exp = _torrent(tmp_path, pl, sizes, 29)
+    _damage(paths, pl)
+    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
+    with HashPool(pl, slots=3, batch_pieces=4, slot_bytes=3 << 20, hooks=True) as pool:
+        for huge in (1, 0, 1):
+            pool.lib.vx_tuning_stage_huge(pool._h, huge)
+            for cold in (False, True):
+                if cold:
+                    for p in paths:
+                        if os.path.exists(p):
+                            bench.drop_cache(p)
+                got, _ = pool.verify_files(paths, sizes, pl, exp, io_threads=3)
+                assert got == want, (huge, cold)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

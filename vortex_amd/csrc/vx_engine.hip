@@ -218,8 +218,11 @@ struct vx_ctx {
     hipStream_t copy_stream = nullptr;
     int verify_copy_stream = 1;
     // How pinned stages are allocated (alloc_stage): 1 = 2 MiB-aligned mmap
-    // with transparent huge pages, then hipHostRegister; 0 = hipHostMalloc.
-    int stage_huge = 0;
+    // with transparent huge pages, then hipHostRegister; 0 = hipHostMalloc
+    // (vx_tuning_stage_huge, test build).  Huge pages: warm re-verify 39.1 ->
+    // 45.2 GiB/s (its H2D copies 44-47 -> 49-50.5), cold 10.9 -> 14.2, median
+    // of 7-9 alternating calls on one box.
+    int stage_huge = 1;
     hipEvent_t anchor_ev = nullptr;            // maps the rounds' GPU times onto the host clock
     uint64_t verify_t0_ns = 0;                 // the running re-verify call's start (steady clock)
 };
