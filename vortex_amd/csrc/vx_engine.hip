@@ -361,6 +361,7 @@ int alloc_slot(Slot& s, uint64_t arena, uint32_t cap) {
 int ensure_stage(const vx_ctx* c, Slot& s) {
     if (s.h_stage) return 0;
     s.h_stage = alloc_stage(s.arena_cap, c->stage_huge != 0, &s.stage_map);
+    if (!s.h_stage && c->stage_huge) s.h_stage = alloc_stage(s.arena_cap, false, &s.stage_map);  // registration refused
     if (!s.h_stage) return fail(VX_ENOMEM, "pinned stage allocation failed");
     return 0;
 }
