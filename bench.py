@@ -419,7 +419,7 @@ def ragged_leg(dev, stream, steps: int = 5):
     floor_valu_us = 405 * 4 / 2.4e9 * 1e6     # rounds only: 405 VALU at one wave's 4-cycle issue, 2.4 GHz
     floor_inst_us = 425 * 4 / 2.4e9 * 1e6     # + the consumer's 20 ds_read_b128 issue slots
     # the generated consumer alone (no producer, no barriers) with its 20-read burst per block:
-    # 1,775 cycles (tools/native/pair_probe.hip no_barriers_idle_producer, profiles/r02/consumer_asm/)
+    # 1,775 cycles (round-2 pair probe, no_barriers_idle_producer: profiles/r02/consumer_asm/, EXPERIMENTS.md §3.2)
     floor_reads_us = 1775.4 / 2.4e9 * 1e6
     del data, d_off, d_len, order, dig, expected, matched
     torch.cuda.empty_cache()

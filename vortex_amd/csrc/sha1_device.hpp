@@ -35,7 +35,7 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int n) {
 // gfx950 each straddle cost about one issue slot.
 // -DVX_XOR2_VOP2 (A/B only): the plain 4-byte VOP2 xor.  Even with 2 or 4 waves per
 // SIMD, where a VOP2 op takes its SIMD half the cycles of a VOP3 one, it was no
-// faster (tools/ab_xor_vop2.sh, profiles/r02/negative/ab_xor_vop2.txt).
+// faster (profiles/r02/negative/ab_xor_vop2.txt).
 #ifdef VX_XOR2_VOP2
 #define VX_XOR2(a, b) ((a) ^ (b))
 #else

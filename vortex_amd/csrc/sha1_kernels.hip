@@ -355,7 +355,7 @@ __device__ __forceinline__ void rounds_regs(State& s, const uint4 (&w)[20]) {
 // generated and checked by tools/gen_sha1_rounds.py): hipcc's own schedule
 // and registers for the rounds ran a lone wave at ~4.5 cycles per VALU,
 // the fixed stream at ~4.06 including the ring reads
-// (tools/native/rounds_sched_probe.hip).  The asm holds the
+// (a round-2 scheduling probe, EXPERIMENTS.md §3.2).  The asm holds the
 // block loop, the ring reads (block b+1's 20 ds_read_b128 in a burst at the
 // top of block b into the other of two word sets), the barriers (1 + nb_wave,
 // as the C++ consumer) and, with kSelect, the ragged phase-2 commit for

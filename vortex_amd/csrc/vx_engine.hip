@@ -507,10 +507,10 @@ int launch_slot(vx_ctx* c, int si) {
 }
 
 // Every eligible slot goes zero-copy: the kernel beats gather + hash
-// everywhere measured (profiles/r03/zero_copy/).  Full async slots (tools/ab_zero_copy.sh, alternating
+// everywhere measured (profiles/r03/zero_copy/).  Full async slots (round-3 A/B, alternating
 // runs of async_probe, one registered mmap per buffer): 16 KiB 33 -> 48
 // GiB/s, 256 / 512 KiB 47.8 -> 48.8 / 48.1 -> 49.0, 1 / 2 / 4 MiB 44 -> 48 /
-// 34 -> 44 / 30 -> 35.  Small, latency-bound batches (tools/loop_latency_ab.py,
+// 34 -> 44 / 30 -> 35.  Small, latency-bound batches (round-3 loop-latency A/B,
 // 32-piece batches) only in the three-wave form: download-loop p50 at 32 KiB
 // 0.68 ms against 0.70, 256 KiB 3.75 against 3.75, 2 MiB 26.6 against 27.7.
 

@@ -121,7 +121,7 @@ struct ReadItem {
 // round 3).  vortex's re-verify (file_store.rs:271-296) preads through the
 // page cache; at startup the torrent's data is usually not cached, and on the
 // MI355X box a buffered cold pread ran 5-12 GiB/s where O_DIRECT of the same
-// file ran ~20 GiB/s (16 threads, tools/disk_probe.sh, profiles/r03/disk/).
+// file ran ~20 GiB/s (16 threads, profiles/r03/disk/; tools/disk_qd_probe.py).
 // Once per call, each file's residency is sampled (mincore on a PROT_READ
 // mapping of the file, which faults nothing in).  A file the page cache holds
 // (nearly) whole is read buffered throughout, and one it (nearly) lacks goes

@@ -7,7 +7,7 @@
 // per-call cost), while a kernel reading the pieces through the device
 // mapping of the registered pool runs at the flat-DMA rate: 53.5 GiB/s for
 // scattered 16 KiB, 256 KiB and 2 MiB pieces alike
-// (tools/native/gather_probe.hip, profiles/r01/h2d/gather.json).
+// (a round-1 probe: profiles/r01/h2d/gather.json).
 //
 // Work is cut into 64 KiB tiles: piece i owns tiles [tfirst[i], tfirst[i+1])
 // (a prefix built at submit; pieces not gathered own none).  A workgroup takes
