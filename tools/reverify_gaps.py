@@ -126,11 +126,12 @@ def cold_ab(a, path, total, n, pl, exp, threads):
     import bench
     from vortex_amd.hash_pool import HashPool
 
-    # "<verify_cold_chunk>[h][@<slot MiB>]": h = huge-page stages (vx_tuning_stage_huge)
+    # "<verify_cold_chunk>[h][@<slot MiB>][x<readers>]": h = huge-page stages (vx_tuning_stage_huge)
     chunks = a.cold.split(",")
-    pools = {}
+    pools, readers = {}, {}
     for ch in chunks:
-        spec, _, mib = ch.partition("@")
+        spec, _, mib = ch.partition("x")[0].partition("@")
+        readers[ch] = int(ch.partition("x")[2] or threads)
         pools[ch] = HashPool(pl, slots=4, slot_bytes=int(mib or 512) << 20, batch_pieces=4096,
                              verify_cold_chunk=int(spec.rstrip("h")), hooks=True)
         pools[ch].lib.vx_tuning_stage_huge(pools[ch]._h, int(spec.endswith("h")))
@@ -141,7 +142,7 @@ def cold_ab(a, path, total, n, pl, exp, threads):
         for ch, pool in pools.items():
             bench.drop_cache(path)
             t0 = time.perf_counter()
-            got, bad = pool.verify_files([path], [total], pl, exp, io_threads=threads)
+            got, bad = pool.verify_files([path], [total], pl, exp, io_threads=readers[ch])
             el = time.perf_counter() - t0
             assert all(got) and bad == 0
             tr = pool.last_verify()
