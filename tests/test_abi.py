@@ -503,12 +503,13 @@ def test_plan_verify_split_host(built):
             assert p.use_gpu == 0 and p.gpu_s == 0 and p.cpu_s == pytest.approx(alone_cpu)
     # config 5 beside a 12-thread pool (the box's 16 threads less the engine's 8 readers' share): the
     # GPU takes most pieces and the two sides meet; measured: 763 pieces on the GPU gave 38 / 48 ms
-    # (GPU / pool side), and 892 the best of three points on two boxes (profiles/r05/split/)
+    # (GPU / pool side), 892 the best of three points on two boxes (profiles/r05/split/), and 944
+    # the best on four HEAD bench runs, 55.6-57.8 GiB/s (refit_r05_bench.json)
     first, count, p = _split(1387, 2 * MiB, 2907832320, 12, rate=2.32e9)
     assert 800 < count < 950 and abs(p.gpu_s - p.cpu_s) < 0.15 * max(p.gpu_s, p.cpu_s)
-    assert 2907832320 / max(p.gpu_s, p.cpu_s) / (1 << 30) == pytest.approx(58, rel=0.1)
-    # and the split is well below the GPU alone
-    assert max(p.gpu_s, p.cpu_s) < 0.85 * _plan_g(1387, 2 * MiB, 2907832320, 16, 1).gpu_s
+    assert 2907832320 / max(p.gpu_s, p.cpu_s) / (1 << 30) == pytest.approx(57, rel=0.1)
+    # and the split is below the GPU alone (measured 15-30 % on the box)
+    assert max(p.gpu_s, p.cpu_s) < 0.9 * _plan_g(1387, 2 * MiB, 2907832320, 16, 1).gpu_s
     # full node: pool alone
     assert _split(1387, 2 * MiB, 2907832320, 128, g=8)[1] == 0
     # one piece and an empty torrent

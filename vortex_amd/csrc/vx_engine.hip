@@ -2182,9 +2182,12 @@ constexpr double kBatchLatency = 1e-3;  // launch, H2D of a small batch, D2H, po
 // the GPU side's bytes move at kSplitLink of the link rate (page-cache reads,
 // stage writes and the DMA share host memory with the pool's hashing).  Fitted
 // to the warm config-5 split over three boxes (profiles/r05/split/: GPU side
-// 36-43 GB/s, the 12-thread pool at 0.85-0.98 of its rate alone; the best of
-// three points was the one with the most GPU pieces on two of them).
-constexpr double kSplitLink = 0.74, kSplitPool = 0.85;
+// 36-43 GB/s, the 12-thread pool at 0.85-0.98 of its rate alone), then refit
+// on four HEAD bench runs with the copy stream and huge-page stages
+// (refit_r05_bench.json: GPU side 38-39.5 GiB/s at its largest share, the pool
+// at 0.74-0.85 of its rate alone, median 0.80; at 0.85 the point with 10 % more
+// GPU pieces won on all four, by 1-16 %).
+constexpr double kSplitLink = 0.74, kSplitPool = 0.80;
 
 // The GPU path over `bytes` bytes of pieces piece_length long, over n_gpus links
 // at `link` of the PCIe rate.
