@@ -619,55 +619,6 @@ def split_call(pool, paths: list, lens: list, n: int, pl: int, exp: bytes, first
             "matched": merged}
 
 
-def shared_call(pool, paths: list, lens: list, n: int, pl: int, exp: bytes, io_threads: int, cpu_threads: int) -> dict:
-    """One bulk re-verify shared by the GPU and vortex's pool with no plan
-    (vx_verify_files_shared, INTEGRATION.md "The shared re-verify"): the pool
-    restatement's threads take pieces from the head of one claim word while
-    the engine hashes, round by round, only the pieces above the head it
-    sees, and fences the pool as its last rounds start.  Both write into one
-    verdict buffer (the Box<[bool]> of torrent.rs:727-740).  Returns wall
-    time, each side's time and pieces, whether every verdict matched, and
-    the verdicts."""
-    import threading
-
-    import oracle
-
-    claim = ctypes.c_uint64(n << 32)
-    out = ctypes.create_string_buffer(max(1, n))
-    res, errs = {}, []
-
-    def gpu():
-        try:
-            t0 = time.perf_counter()
-            boundary, bad = pool.verify_files_shared(paths, lens, pl, exp, claim, out, io_threads=io_threads)
-            res["gpu"] = (time.perf_counter() - t0, boundary, bad)
-        except Exception as e:  # noqa: BLE001  (raised below, on the calling thread)
-            errs.append(e)
-
-    def cpu():
-        try:
-            t0 = time.perf_counter()
-            k = oracle.pool_verify_files_claim(paths, lens, pl, exp, cpu_threads, claim, 0, out)
-            res["cpu"] = (time.perf_counter() - t0, k)
-        except Exception as e:  # noqa: BLE001
-            errs.append(e)
-
-    th = [threading.Thread(target=gpu), threading.Thread(target=cpu)]
-    t0 = time.perf_counter()
-    for t in th:
-        t.start()
-    for t in th:
-        t.join()
-    wall = time.perf_counter() - t0
-    if errs:
-        raise errs[0]
-    matched = [bool(b) for b in out.raw[:n]]
-    boundary = res["gpu"][1]
-    assert res["cpu"][1] == boundary, "shared re-verify: the pool's pieces are not exactly [0, boundary)"
-    return {"s": wall, "gpu_s": res["gpu"][0], "cpu_s": res["cpu"][0], "gpu_first": boundary,
-            "ok": all(matched) and res["gpu"][2] == 0, "matched": matched}
-
-
 def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
     """BASELINE config 5: full re-verify of a torrent's data from disk with
     the linux-mint geometry (cli/linux-mint.torrent: 2,907,832,320 B, 2 MiB
@@ -758,24 +709,14 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
             points = sorted({n - k0, n - int(k0 * 0.9), max(0, n - int(k0 * 1.1))}) if k0 else [n]
             # The points alternate call by call with the GPU alone (all readers) and the pool
             # alone (all threads) as references, so a box's drift lands on all of them alike.
-            # (first = -1: the shared re-verify, no plan: vx_verify_files_shared beside the claiming pool)
-            cfgs = [(first, io_t, pool_t) for first in points] + [(0, threads, threads), (n, threads, threads),
-                                                                  (-1, io_t, pool_t)]
+            cfgs = [(first, io_t, pool_t) for first in points] + [(0, threads, threads), (n, threads, threads)]
             by_cfg = {c: [] for c in cfgs}
             for _ in range(split_reps):
                 for c in cfgs:
-                    by_cfg[c].append(shared_call(pool, [path], [total], n, pl, exp, c[1], c[2]) if c[0] < 0 else
-                                     split_call(pool, [path], [total], n, pl, exp, c[0], c[1], c[2]))
+                    by_cfg[c].append(split_call(pool, [path], [total], n, pl, exp, c[0], c[1], c[2]))
             for (first, io_c, pool_c), calls in by_cfg.items():
                 assert all(c["ok"] for c in calls), "split re-verify: a verdict differs from the expected table"
                 med = sorted(calls, key=lambda c: c["s"])[len(calls) // 2]
-                if first < 0:
-                    split["shared"] = {"io_threads": io_c, "cpu_threads": pool_c,
-                                       "value": round(total / med["s"] / GiB, 2),
-                                       "s_runs": [round(c["s"], 4) for c in calls],
-                                       "gpu_first_runs": [c["gpu_first"] for c in calls],
-                                       "gpu_s": round(med["gpu_s"], 4), "cpu_s": round(med["cpu_s"], 4)}
-                    continue
                 entry = {"io_threads": io_c, "cpu_threads": pool_c, "gpu_first": first,
                          "planned": first == n - k0 and io_c == io_t, "value": round(total / med["s"] / GiB, 2),
                          "s_runs": [round(c["s"], 4) for c in calls],
@@ -841,7 +782,6 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
                   "gpu_only": split["gpu_alone"]["value"], "pool_only": split["pool_alone"]["value"],
                   # against the better of each side's two figures: in the alternation and in the legs above
                   "beats_both": pv > either, "best_beats_both": best["value"] > either,
-                  "shared_value": split["shared"]["value"], "shared_beats_both": split["shared"]["value"] > either,
                   "pool_kind": "port",
                   "sample": f"the warm file split at GPU pieces [first, {n}) via vx_verify_files_range while the CPU "
                             f"pool restatement (vortex's par_iter stand-in, 3/4 of the {threads} threads) verifies "

@@ -310,23 +310,6 @@ int64_t vx_verify_files(vx_ctx* ctx, const char* const* paths, const uint64_t* f
 int64_t vx_verify_files_range(vx_ctx* ctx, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
                               uint32_t piece_length, const uint8_t* expected, size_t n_pieces, size_t first,
                               size_t count, uint8_t* matched_out, uint32_t io_threads);
-/* The same re-verify shared with the caller's own pool, at once, with no
- * model: *claim is one 64-bit word, head (low 32 bits) | stop (high 32), set
- * by the caller to first | (end << 32) before the call.  The caller's pool
- * threads take pieces from the head while head < stop, each with one
- * compare-and-swap of the word (head + 1), and verify them themselves (the
- * par_iter body of torrent.rs:724-740); the engine reads and hashes, round by
- * round, only the pieces at or above the head it sees, so its share shrinks
- * as the pool advances, and it fences the pool (stop = head) as its last
- * rounds start.  On return the word's head is the boundary: matched_out
- * (end - first bytes, matched_out[k] for piece first+k) holds the engine's
- * verdicts from there on and is not written below it, where the pool's go;
- * the return value counts I/O errors among the engine's pieces only.  Always
- * the chunk rounds (INTEGRATION.md "The shared re-verify").
- * Pieces up to 2^32 - 1. */
-int64_t vx_verify_files_shared(vx_ctx* ctx, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
-                               uint32_t piece_length, const uint8_t* expected, size_t n_pieces, uint64_t* claim,
-                               uint8_t* matched_out, uint32_t io_threads);
 /* In-process multi-GPU re-verify: vortex is one process with one event loop
  * (event_loop.rs:385), so on a multi-GPU host it holds one context per GPU
  * (vx_config.device) and hands them all to this call, which replaces the

@@ -65,10 +65,6 @@ def lib() -> ctypes.CDLL:
                                             ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_void_p]
         L.vxo_pool_verify_files.restype = ctypes.c_int
-        L.vxo_pool_verify_files_claim.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
-                                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                                                  ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64, ctypes.c_void_p]
-        L.vxo_pool_verify_files_claim.restype = ctypes.c_int
         L.vxo_sha1_ctx_size.restype = ctypes.c_size_t
         L.vxo_sha1_init.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.vxo_sha1_update.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
@@ -164,18 +160,6 @@ def pool_verify_files(paths, file_lengths, piece_length: int, expected: bytes, t
     out = ctypes.create_string_buffer(max(1, n))
     lib().vxo_pool_verify_files(arr, lens, len(paths), piece_length, exp, n, threads, backend, out)
     return [bool(b) for b in out.raw[:n]]
-
-
-def pool_verify_files_claim(paths, file_lengths, piece_length: int, expected: bytes, threads: int,
-                            claim: ctypes.c_uint64, base: int, out, backend: int = 0) -> int:
-    """The pool beside vx_verify_files_shared: its threads take pieces from
-    the head of `claim` (head | stop << 32, one compare-and-swap each) while
-    head < stop and write out[i - base].  Returns the pieces it verified."""
-    arr = (ctypes.c_char_p * max(1, len(paths)))(*[p.encode() for p in paths])
-    lens = (ctypes.c_uint64 * max(1, len(file_lengths)))(*file_lengths)
-    exp = ctypes.create_string_buffer(expected, max(1, len(expected)))
-    return lib().vxo_pool_verify_files_claim(arr, lens, len(paths), piece_length, exp, threads, backend,
-                                             ctypes.byref(claim), base, out)
 
 
 # ---------------------------------------------------------------- geometry

@@ -166,34 +166,8 @@ void vxo_sha1_init(void* c, int backend);
 void vxo_sha1_update(void* c, const uint8_t* p, size_t n);
 void vxo_sha1_final(void* c, uint8_t out[20]);
 
-namespace {
-int pool_verify_files_impl(const char* const* paths, const uint64_t* lens, size_t nfiles, uint32_t piece_length,
-                           const uint8_t* expected, size_t n, int threads, int backend, uint8_t* matched_out,
-                           uint64_t* claim, uint64_t base);
-}
-
 int vxo_pool_verify_files(const char* const* paths, const uint64_t* lens, size_t nfiles, uint32_t piece_length,
                           const uint8_t* expected, size_t n, int threads, int backend, uint8_t* matched_out) {
-    return pool_verify_files_impl(paths, lens, nfiles, piece_length, expected, n, threads, backend, matched_out,
-                                  nullptr, 0);
-}
-
-// The same pool beside vx_verify_files_shared (include/vx_hash.h): its
-// threads take pieces from the head of *claim (head | stop << 32) with one
-// compare-and-swap each while head < stop, and write matched_out[i - base].
-// Returns the number of pieces it verified.
-int vxo_pool_verify_files_claim(const char* const* paths, const uint64_t* lens, size_t nfiles,
-                                uint32_t piece_length, const uint8_t* expected, int threads, int backend,
-                                uint64_t* claim, uint64_t base, uint8_t* matched_out) {
-    return pool_verify_files_impl(paths, lens, nfiles, piece_length, expected, 0, threads, backend, matched_out,
-                                  claim, base);
-}
-}  // extern "C"
-
-namespace {
-int pool_verify_files_impl(const char* const* paths, const uint64_t* lens, size_t nfiles, uint32_t piece_length,
-                           const uint8_t* expected, size_t n, int threads, int backend, uint8_t* matched_out,
-                           uint64_t* claim, uint64_t base) {
     struct Span { int64_t sp, so, ep, eo, len; };
     std::vector<Span> fs;
     int64_t sp = 0, so = 0;
@@ -234,37 +208,13 @@ int pool_verify_files_impl(const char* const* paths, const uint64_t* lens, size_
         }
         vxo_sha1_final(ctx.data(), p.digest);
         p.hash_matched = ok && std::memcmp(p.digest, expected + 20 * idx, 20) == 0;
-        if (claim)
-            matched_out[idx - base] = p.hash_matched ? 1 : 0;  // pieces taken from the head, written in place
-        else
-            result[idx] = p.hash_matched ? 1 : 0;
+        result[idx] = p.hash_matched ? 1 : 0;
         return p;
     };
-    int taken = 0;
-    if (claim) {
-        std::atomic<int> count{0};
-        std::vector<std::thread> ws;
-        for (int t = 0; t < std::max(1, threads); ++t)
-            ws.emplace_back([&] {
-                uint64_t w = __atomic_load_n(claim, __ATOMIC_ACQUIRE);
-                for (;;) {
-                    const uint64_t h = w & 0xffffffffull, stop = w >> 32;
-                    if (h >= stop) break;
-                    if (!__atomic_compare_exchange_n(claim, &w, w + 1, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE))
-                        continue;  // w reloaded: another thread or the engine's fence moved it
-                    (void)job((size_t)h);
-                    count.fetch_add(1, std::memory_order_relaxed);
-                    w = __atomic_load_n(claim, __ATOMIC_ACQUIRE);
-                }
-            });
-        for (auto& w : ws) w.join();
-        taken = count.load();
-    } else {
-        run_pool(n, threads, job, ch);
-        std::memcpy(matched_out, result.data(), n);
-    }
+    run_pool(n, threads, job, ch);
     for (int fd : fds)
         if (fd >= 0) close(fd);
-    return claim ? taken : 0;
+    std::memcpy(matched_out, result.data(), n);
+    return 0;
 }
-}  // namespace
+}  // extern "C"

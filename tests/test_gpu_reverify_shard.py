@@ -94,57 +94,6 @@ def test_split_verify_with_the_pool(built, gpu, tmp_path, pl):
             assert r["ok"] is False  # the damaged pieces mismatch on whichever side holds them
 
 
-@pytest.mark.parametrize("pl", [64 * 1024, 256 * 1024, 1 << 20])
-def test_shared_verify_with_a_claiming_pool(built, gpu, tmp_path, pl):
-    """vx_verify_files_shared (include/vx_hash.h): the CPU pool restatement's
-    threads take pieces from the head of one claim word while the engine
-    hashes only the pieces above the head it sees and fences the pool; one
-    verdict buffer.  On a damaged multi-file torrent, for pools of 0-6
-    threads (0: the engine alone; 6 on 64 KiB pieces: the pool takes most)
-    and for sub-ranges, every verdict equals the pool restatement's over the
-    whole range, the pool took exactly [first, boundary), and the I/O-error
-    count covers the engine's pieces only."""
-    import ctypes
-    import threading
-
-    from vortex_amd._lib import VX_EINVAL, VxError
-    from vortex_amd.hash_pool import HashPool
-
-    sizes = [3, 4 * pl + 17, 2 * pl, 0, 3 * pl - 5, pl + 1, 64, 2 * pl + pl // 2] + [5 * pl] * 4
-    paths, exp = _torrent(tmp_path, pl, sizes, 31)
-    n = len(exp) // 20
-    _damage(paths, pl)
-    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
-    assert not all(want) and any(want)
-    with HashPool(pl, slots=3, batch_pieces=4, slot_bytes=4 << 20) as pool:
-        for first, end, threads in [(0, n, 0), (0, n, 1), (0, n, 2), (0, n, 6), (3, n - 2, 2), (n - 1, n, 1),
-                                    (5, 5, 1)]:
-            claim = ctypes.c_uint64(first | (end << 32))
-            out = ctypes.create_string_buffer(b"\x09" * max(1, end - first))
-            got = {}
-
-            def cpu():
-                got["k"] = oracle.pool_verify_files_claim(paths, sizes, pl, exp, threads, claim, first, out)
-
-            th = threading.Thread(target=cpu) if threads else None
-            if th:
-                th.start()
-            boundary, bad = pool.verify_files_shared(paths, sizes, pl, exp, claim, out, io_threads=3)
-            if th:
-                th.join()
-            if end == first:
-                assert boundary == first and bad == 0
-                continue
-            assert first <= boundary <= end and claim.value >> 32 == boundary, (first, end, threads)
-            assert got.get("k", 0) == boundary - first
-            assert [bool(b) for b in out.raw[:end - first]] == want[first:end], (first, end, threads, boundary)
-            assert 0 <= bad <= end - boundary
-        with pytest.raises(VxError) as e:
-            pool.verify_files_shared(paths, sizes, pl, exp, ctypes.c_uint64(2 | (n + 1) << 32),
-                                     ctypes.create_string_buffer(n + 1))
-        assert e.value.code == VX_EINVAL
-
-
 @pytest.mark.parametrize("pl", [256 * 1024, 1 << 20])
 def test_stage_memory_kinds(built, gpu, tmp_path, pl):
     """The pinned stages the readers fill: huge-page mappings registered with

@@ -157,35 +157,6 @@ def test_pool_verify_files_restatement(tmp_path):
         assert got[i] == (not touches_bad), i
 
 
-def test_pool_verify_files_claim(tmp_path):
-    """The pool beside vx_verify_files_shared (oracle pool_verify_files_claim):
-    threads take pieces from the claim word's head while head < stop; every
-    piece of [first, stop) is verified exactly once (two pools racing on one
-    word included), written at out[i - first], and the head ends at stop."""
-    import ctypes
-    import threading
-
-    sizes = [64, 100, 0, 5000, 32768, 3, 40000]
-    pl = 4096
-    paths = _write_files(tmp_path, sizes)
-    exp = _expected_from_concat(paths, sizes, pl)
-    n = len(exp) // 20
-    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=2)
-    for first, stop, pools in [(0, n, 1), (2, n - 3, 1), (0, n, 2), (4, 4, 1)]:
-        claim = ctypes.c_uint64(first | (stop << 32))
-        out = ctypes.create_string_buffer(b"\x09" * (n - first + 1))
-        counts = []
-        th = [threading.Thread(target=lambda: counts.append(
-            oracle.pool_verify_files_claim(paths, sizes, pl, exp, 3, claim, first, out))) for _ in range(pools)]
-        for t in th:
-            t.start()
-        for t in th:
-            t.join()
-        assert sum(counts) == stop - first and claim.value == stop | (stop << 32)
-        assert [bool(b) for b in out.raw[:stop - first]] == want[first:stop]
-        assert out.raw[stop - first:n - first] == b"\x09" * (n - stop)  # past stop: untouched
-
-
 def _layout_ids(golden_path=os.path.join(os.path.dirname(__file__), "golden", "vectors.json")):
     import json
 

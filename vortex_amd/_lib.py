@@ -41,8 +41,7 @@ EXPORTS = (
     "vx_abi_version", "vx_last_error", "vx_strerror", "vx_device_count", "vx_config_default",
     "vx_create", "vx_destroy", "vx_register_host_buffer", "vx_unregister_host_buffer",
     "vx_submit", "vx_flush", "vx_poll", "vx_drain", "vx_pending", "vx_set_piece_table", "vx_submit_piece",
-    "vx_sha1_batch", "vx_verify_batch", "vx_verify_files", "vx_verify_files_range", "vx_verify_files_shared",
-    "vx_verify_files_multi",
+    "vx_sha1_batch", "vx_verify_batch", "vx_verify_files", "vx_verify_files_range", "vx_verify_files_multi",
     "vx_sha1_device_uniform", "vx_sha1_device_ragged", "vx_sha1_device_ragged_hint", "vx_sort_order",
     "vx_plan_verify", "vx_plan_verify_gpus", "vx_plan_verify_split", "vx_get_stats", "vx_reset_stats",
     "vx_last_verify", "vx_last_verify_rounds",
@@ -152,8 +151,6 @@ def _declare(L: ctypes.CDLL, tuning: bool = False) -> None:
                                    c.c_uint32], c.c_int64),
         "vx_verify_files_multi": ([vp, c.c_size_t, vp, vp, c.c_size_t, c.c_uint32, vp, c.c_size_t, vp, c.c_uint32],
                                   c.c_int64),
-        "vx_verify_files_shared": ([vp, vp, vp, c.c_size_t, c.c_uint32, vp, c.c_size_t, c.POINTER(c.c_uint64), vp,
-                                    c.c_uint32], c.c_int64),
         "vx_sha1_device_uniform": ([vp, c.c_uint64, c.c_uint32, c.c_uint32, vp, vp, vp, vp], c.c_int),
         "vx_sha1_device_ragged": ([vp, vp, vp, vp, c.c_uint32, vp, vp, vp, vp], c.c_int),
         "vx_sha1_device_ragged_hint": ([vp, vp, vp, vp, c.c_uint32, c.c_uint32, c.c_uint64, vp, vp, vp, vp],

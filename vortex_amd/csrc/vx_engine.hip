@@ -1409,25 +1409,21 @@ struct ChunkPipe {
     // Wait for every round, then copy verdicts / digests back (either may be
     // NULL).  bad (may be NULL): pieces the caller fails for an I/O error,
     // counted in io_errors and not again as mismatches.
-    // from: rows [0, from) are not this call's (a shared re-verify's pool took
-    // them): their verdicts are neither copied out nor counted.
-    int finish(uint8_t* matched_out, uint8_t* digests_out, int rc, const uint8_t* bad = nullptr, uint64_t from = 0) {
+    int finish(uint8_t* matched_out, uint8_t* digests_out, int rc, const uint8_t* bad = nullptr) {
         if (!rc) {
             for (auto& s : c->slots)
                 if (s.state == Slot::INFLIGHT && hipEventSynchronize(s.done) != hipSuccess) rc = VX_EDEVICE;
             if (rc) (void)fail(rc, "chunk rounds failed on device");
         }
-        if (!rc && matched_out && d_match && from < cnt &&
-            hipMemcpy(matched_out + from, d_match + from, cnt - from, hipMemcpyDeviceToHost) != hipSuccess)
+        if (!rc && matched_out && d_match && hipMemcpy(matched_out, d_match, cnt, hipMemcpyDeviceToHost) != hipSuccess)
             rc = fail(VX_EDEVICE, "verdict D2H failed");
         if (!rc && digests_out && hipMemcpy(digests_out, d_dig, cnt * 20, hipMemcpyDeviceToHost) != hipSuccess)
             rc = fail(VX_EDEVICE, "digest D2H failed");
         if (!rc) {
-            c->stats.pieces_completed += cnt - std::min(from, cnt);
+            c->stats.pieces_completed += cnt;
             c->stats.bytes_completed += bytes;
             if (matched_out && d_match)
-                for (uint64_t i = from; i < cnt; ++i)
-                    c->stats.pieces_mismatched += matched_out[i] == 0 && !(bad && bad[i]);
+                for (uint64_t i = 0; i < cnt; ++i) c->stats.pieces_mismatched += matched_out[i] == 0 && !(bad && bad[i]);
         }
         for (auto& s : c->slots)
             if (s.state == Slot::INFLIGHT) {
@@ -1488,40 +1484,15 @@ std::vector<std::pair<uint64_t, uint64_t>> chunk_schedule(uint64_t L, uint64_t C
 // every round whose read outlasted the previous copy left PCIe idle (the head
 // ramp's doubling rounds most of all).  Each round's data
 // copy is timed on the GPU (vx_tuning_last_verify).
-//
-// claim (vx_verify_files_shared): a word the caller's pool updates at the same
-// time, head (low 32 bits: the pool's next piece) | stop (high 32: where the
-// pool must stop).  The pool takes pieces from the head while head < stop;
-// every round reads and hashes only the pieces at or above the head it sees,
-// so the GPU's share shrinks as the pool advances, and a round that starts the
-// last kFence rounds fences the pool (stop = head).  Pieces below the final
-// head are the pool's; the engine's verdicts start there (*from_out).
 int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t pl, uint64_t total, uint64_t first,
-                   uint64_t end, uint64_t C, uint64_t* claim = nullptr, uint64_t* from_out = nullptr) {
+                   uint64_t end, uint64_t C) {
     vx_ctx* c = fv.c;
     const uint64_t last_len = total - (n - 1) * (uint64_t)pl;
     const uint64_t cnt = end - first;
     ChunkPipe cp(c);
     int rc = cp.open(cnt, fv.expected + 20 * first, "vx_verify_files");
     if (!rc && c->verify_copy_stream) rc = cp.use_copy_stream();
-    auto range_bytes = [&](uint64_t a) {  // piece bytes of [a, end)
-        return a >= end ? 0 : (end - a) * (uint64_t)pl - (end == n ? (uint64_t)pl - last_len : 0);
-    };
-    cp.bytes = range_bytes(first);
-    constexpr size_t kFence = 3;
-    uint64_t from = first;  // the engine's first piece: first, or the head at the fence
-    bool fenced = claim == nullptr;
-    auto fence = [&] {
-        uint64_t w = __atomic_load_n(claim, __ATOMIC_ACQUIRE);
-        for (;;) {
-            const uint64_t h = w & 0xffffffffull;
-            if (__atomic_compare_exchange_n(claim, &w, h | (h << 32), false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) {
-                from = std::min<uint64_t>(std::max<uint64_t>(h, first), end);
-                break;
-            }
-        }
-        fenced = true;
-    };
+    cp.bytes = cnt * (uint64_t)pl - (end == n ? (uint64_t)pl - last_len : 0);
     // windows of W pieces; each window runs its rounds in order
     const Slot& s0 = c->slots[0];
     const uint64_t W = std::max<uint64_t>(1, std::min<uint64_t>(s0.cap, s0.arena_cap / C));
@@ -1574,10 +1545,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     auto consume = [&] { fv.consume(); };
     // Reserve a slot for round r and queue its reads; false when no slot is
     // free and `block` is not set.
-    auto start_read = [&](Round& r, size_t idx, bool block) -> bool {
-        if (!fenced && idx + kFence >= rounds.size()) fence();
-        // pieces below the pool's head are the pool's: not read, not hashed
-        const uint64_t head = fenced ? from : std::max<uint64_t>(first, __atomic_load_n(claim, __ATOMIC_ACQUIRE) & 0xffffffffull);
+    auto start_read = [&](Round& r, bool block) -> bool {
         int si = -1;
         if (block) {
             si = cp.free_slot(consume);
@@ -1594,7 +1562,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
         auto& it = items[si];
         it.clear();
         uint32_t m = 0;
-        for (uint64_t i = std::max(r.w0, head); i < r.w1; ++i) {
+        for (uint64_t i = r.w0; i < r.w1; ++i) {
             const uint64_t len_i = i == n - 1 ? last_len : pl;
             if (r.a >= len_i && !(r.a == 0 && len_i == 0)) continue;  // piece already finished
             const uint64_t clen = std::min<uint64_t>(r.len, len_i - r.a);
@@ -1617,7 +1585,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     };
     size_t nr = 0;  // next round to read
     for (size_t ne = 0; ne < rounds.size() && !rc; ++ne) {
-        while (nr < rounds.size() && nr <= ne + depth && start_read(rounds[nr], nr, nr == ne)) ++nr;
+        while (nr < rounds.size() && nr <= ne + depth && start_read(rounds[nr], nr == ne)) ++nr;
         if (rc) break;
         Round& r = rounds[ne];
         if (r.m == 0) continue;
@@ -1661,10 +1629,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
             reset_fill(sl);
             sl.state = Slot::FREE;
         }
-    if (!fenced) fence();  // fewer rounds than kFence, or an error: the pool stops here
-    cp.bytes = range_bytes(from);
-    if (from_out) *from_out = from;
-    rc = cp.finish(fv.matched_out, nullptr, rc, fv.bad.data(), from - first);
+    rc = cp.finish(fv.matched_out, nullptr, rc, fv.bad.data());
     vx_verify_trace& vt = c->last_verify;
     vt.tail_ms = ms(t_last_enqueue, clk::now());
     if (!rc && timed) {  // finish() waited for every round: the copy events are complete
@@ -1691,7 +1656,7 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
     }
     c->last_rounds = std::move(tl);
     if (!rc)
-        for (uint64_t i = from - first; i < cnt; ++i)
+        for (uint64_t i = 0; i < cnt; ++i)
             if (fv.bad[i]) fv.matched_out[i] = 0;
     fv.done = cnt;
     return rc;
@@ -1976,14 +1941,9 @@ int vx_verify_batch(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens,
 }
 
 
-}  // extern "C"
-
-namespace {
-// vx_verify_files_range and, with claim, vx_verify_files_shared (always the
-// chunk rounds: the pool's head is checked round by round).
-int64_t verify_files_impl(vx_ctx* c, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
-                          uint32_t piece_length, const uint8_t* expected, size_t n_pieces, size_t first,
-                          size_t count, uint8_t* matched_out, uint32_t io_threads, uint64_t* claim) {
+int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
+                              uint32_t piece_length, const uint8_t* expected, size_t n_pieces, size_t first,
+                              size_t count, uint8_t* matched_out, uint32_t io_threads) {
     if (!c || (nfiles && (!paths || !file_lengths)) || piece_length == 0 || (n_pieces && !expected) ||
         (count && !matched_out))
         return fail(VX_EINVAL, "vx_verify_files: bad argument");
@@ -1997,7 +1957,7 @@ int64_t verify_files_impl(vx_ctx* c, const char* const* paths, const uint64_t* f
         return fail(VX_EINVAL, "vx_verify_files: n_pieces does not match the files' total length");
     if (count == 0) return 0;
     const uint64_t C = verify_chunk_for(c, count);
-    bool chunked = piece_length >= 2 * C || claim;
+    bool chunked = piece_length >= 2 * C;
     if (piece_length > c->cfg.max_piece_len) chunked = true;  // whole pieces would not fit a slot
     if (chunked ? c->slots[0].arena_cap < C : piece_length > c->cfg.max_piece_len)
         return fail(VX_ERANGE, "vx_verify_files: pieces do not fit the context's slots");
@@ -2014,8 +1974,7 @@ int64_t verify_files_impl(vx_ctx* c, const char* const* paths, const uint64_t* f
     for (size_t f = 0; f < nfiles; ++f) fds[f] = open(paths[f], O_RDONLY | O_CLOEXEC);
     const int nthreads = io_threads ? (int)io_threads : (int)std::max(1u, std::min(16u, usable_cpus()));
     std::vector<uint8_t> bad(count, 0);
-    if (!claim) std::memset(matched_out, 0, count);  // shared: the pool writes the head's verdicts meanwhile
-    uint64_t from = first;
+    std::memset(matched_out, 0, count);
     {
         const vx_files::DirectIo dio(fds, c->cfg.direct_io != 0);
         vx_files::Readers rd(nthreads, fs, fds, piece_length, bad.data(), first, &dio);
@@ -2029,7 +1988,7 @@ int64_t verify_files_impl(vx_ctx* c, const char* const* paths, const uint64_t* f
                                 ? Cc
                                 : C;
         c->last_verify.chunk_bytes = chunked ? Cv : 0;
-        rc = chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total, first, end, Cv, claim, &from)
+        rc = chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total, first, end, Cv)
                      : verify_whole(fv, rd, n_pieces, piece_length, total, first, end);
         if (!rc && !chunked) {
             while (fv.done < count && !rc) {
@@ -2069,31 +2028,9 @@ int64_t verify_files_impl(vx_ctx* c, const char* const* paths, const uint64_t* f
     c->last_verify.wall_ms = (vx_files::Readers::now_ns() - t_call) * 1e-6;
     if (rc) return rc;
     int64_t nbad = 0;
-    for (uint64_t i = from - first; i < count; ++i) nbad += bad[i];  // the engine's pieces only
+    for (uint8_t x : bad) nbad += x;
     c->stats.io_errors += (uint64_t)nbad;
     return nbad;
-}
-}  // namespace
-
-extern "C" {
-
-int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
-                              uint32_t piece_length, const uint8_t* expected, size_t n_pieces, size_t first,
-                              size_t count, uint8_t* matched_out, uint32_t io_threads) {
-    return verify_files_impl(c, paths, file_lengths, nfiles, piece_length, expected, n_pieces, first, count,
-                             matched_out, io_threads, nullptr);
-}
-
-int64_t vx_verify_files_shared(vx_ctx* c, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
-                               uint32_t piece_length, const uint8_t* expected, size_t n_pieces, uint64_t* claim,
-                               uint8_t* matched_out, uint32_t io_threads) {
-    if (!claim) return fail(VX_EINVAL, "vx_verify_files_shared: NULL claim");
-    const uint64_t w = __atomic_load_n(claim, __ATOMIC_ACQUIRE);
-    const uint64_t h0 = w & 0xffffffffull, e = w >> 32;
-    if (h0 > e || e > n_pieces) return fail(VX_EINVAL, "vx_verify_files_shared: claim outside the torrent");
-    if (h0 == e) return 0;
-    return verify_files_impl(c, paths, file_lengths, nfiles, piece_length, expected, n_pieces, h0, e - h0,
-                             matched_out, io_threads, claim);
 }
 
 int64_t vx_verify_files(vx_ctx* c, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,

@@ -303,24 +303,6 @@ class HashPool:
         shard, vx_verify_files_range); the verdicts then cover that range."""
         return _verify_files(self, paths, file_lengths, piece_length, expected, io_threads, first, count)
 
-    def verify_files_shared(self, paths: Sequence[str], file_lengths: Sequence[int], piece_length: int,
-                            expected: bytes, claim: ctypes.c_uint64, out, io_threads: int = 0) -> tuple[int, int]:
-        """The re-verify shared with the caller's own pool at once
-        (vx_verify_files_shared): `claim` holds first | (end << 32) and the
-        caller's pool threads take pieces from its head meanwhile, one
-        compare-and-swap each, while head < stop (bits 32-63); `out` (end -
-        first bytes, writable) gets the engine's verdicts from the final head
-        on, the pool's below it.  Returns (boundary, pieces with I/O errors
-        among the engine's)."""
-        n = len(expected) // 20
-        arr = (ctypes.c_char_p * max(1, len(paths)))(*[os.fsencode(p) for p in paths])
-        lens = (ctypes.c_uint64 * max(1, len(file_lengths)))(*file_lengths)
-        exp = ctypes.create_string_buffer(bytes(expected), max(1, len(expected)))
-        rc = self.lib.vx_verify_files_shared(self._h, arr, lens, len(paths), piece_length, exp, n,
-                                             ctypes.byref(claim), out, io_threads)
-        bad = check(rc, "vx_verify_files_shared", self.lib)
-        return int(claim.value & 0xFFFFFFFF), int(bad)
-
     def verify_batch(self, pieces: Sequence, expected: Sequence[bytes]) -> tuple[list[bool], list[bytes]]:
         n = len(pieces)
         if len(expected) != n:
