@@ -358,7 +358,8 @@ int vx_plan_verify_gpus(uint64_t n_pieces, uint32_t piece_length, uint64_t total
  * vx_verify_files_range / _multi over the GPUs' range): the GPUs take the
  * contiguous tail [*gpu_first, n_pieces), *gpu_count pieces, chosen so the
  * predicted GPU time (the same model over n_gpus, its bytes at 0.74 of the
- * link: the pool shares host memory) meets the pool's time on the rest.
+ * link: the pool shares host memory) meets the pool's time on the rest (at
+ * 0.80 of cpu_thread_rate: the engine's readers share it too).
  * cpu_threads is the pool that runs beside the engine: leave the engine's
  * readers their cores (e.g. 12 pool threads beside 8 readers on 16 cores;
  * INTEGRATION.md "The split").  *gpu_count is 0 when no split beats the pool
