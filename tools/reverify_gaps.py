@@ -126,15 +126,17 @@ def cold_ab(a, path, total, n, pl, exp, threads):
     import bench
     from vortex_amd.hash_pool import HashPool
 
-    # "<verify_cold_chunk>[h][@<slot MiB>][x<readers>]": h = huge-page stages (vx_tuning_stage_huge)
+    # "<verify_cold_chunk>[h][w][@<slot MiB>][x<readers>]": h = huge-page stages (vx_tuning_stage_huge),
+    # w = whole pieces (verify_chunk above half the piece: the whole-piece slots)
     chunks = a.cold.split(",")
     pools, readers = {}, {}
     for ch in chunks:
         spec, _, mib = ch.partition("x")[0].partition("@")
         readers[ch] = int(ch.partition("x")[2] or threads)
+        extra = {"verify_chunk": 2 * pl} if "w" in spec else {}
         pools[ch] = HashPool(pl, slots=4, slot_bytes=int(mib or 512) << 20, batch_pieces=4096,
-                             verify_cold_chunk=int(spec.rstrip("h")), hooks=True)
-        pools[ch].lib.vx_tuning_stage_huge(pools[ch]._h, int(spec.endswith("h")))
+                             verify_cold_chunk=int(spec.rstrip("hw")), hooks=True, **extra)
+        pools[ch].lib.vx_tuning_stage_huge(pools[ch]._h, int("h" in spec))
     res = {ch: [] for ch in chunks}
     for ch, pool in pools.items():
         pool.verify_files([path], [total], pl, exp, io_threads=threads)
@@ -149,7 +151,7 @@ def cold_ab(a, path, total, n, pl, exp, threads):
             bench.drop_cache(path)
             disk = bench.disk_direct_rate(path, total, threads)
             res[ch].append({"GiBps": round(total / el / (1 << 30), 2), "disk_GiBps": disk and round(disk, 2),
-                            "chunk_bytes": tr["chunk_bytes"], "copy_busy_frac": round(tr["copy_busy_frac"], 3),
+                            "chunk_bytes": tr["chunk_bytes"], "copy_busy_frac": tr["copy_busy_frac"] and round(tr["copy_busy_frac"], 3),
                             "read_GiBps": round(tr["read_GiBps"], 2)})
     for p in pools.values():
         p.close()
