@@ -43,6 +43,13 @@ roofline.valu.clock_run: the shader clock of each XCC over the timed steps
 (s_memtime / s_memrealtime stamps, vortex_amd/csrc/vx_clock.hip) and the
 kernel's issue fraction at that clock.
 
+Output: stdout carries ONE compact JSON line of at most 8 KB (compact_line:
+the headline, config, roofline scalars, cpu_baseline, parity, per-rank
+scalars, each leg's scalars); the full record — traces, timelines, the split
+sweep, the nested roofline.valu block, rank identities — goes to the side
+file the line names in `detail` (bench_detail.json beside bench.py, or
+--detail PATH).
+
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
 N > 1: either launched by the driver as
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -1189,6 +1196,82 @@ def roofline(n: int, plen: int, kern_ms: float, achieved: float, workload: str, 
                              "128 KiB) run no faster (DESIGN.md §4)"}}
 
 
+LINE_LIMIT = 8192  # bytes: the stdout line the driver parses (a 23 KB line was lost)
+LEGS = ("ragged", "e2e", "e2e_async", "e2e_contiguous", "reverify", "reverify_cold", "reverify_multi")
+_PROSE = ("sample", "note", "bound_note", "source")  # explanations: the side file keeps them
+
+
+def _scalars(d: dict, depth: int, prefix: str = "", maxlen: int = 96) -> dict:
+    """The scalar fields of `d` (numbers, bools, None, short strings), and of
+    its nested dicts down to `depth` more levels as dotted keys; lists of up
+    to 8 numbers stay.  Errors are always kept (cut to 240 characters)."""
+    out = {}
+    for k, v in d.items():
+        key = prefix + k
+        if k == "error" and v is not None:
+            out[key] = str(v)[:240]
+        elif k in _PROSE:
+            continue
+        elif v is None or isinstance(v, (bool, int, float)):
+            out[key] = v
+        elif isinstance(v, str):
+            if len(v) <= maxlen:
+                out[key] = v
+        elif isinstance(v, list):
+            if len(v) <= 8 and all(x is None or isinstance(x, (int, float)) for x in v):
+                out[key] = v
+        elif isinstance(v, dict) and depth > 0:
+            out.update(_scalars(v, depth - 1, key + ".", maxlen))
+    return out
+
+
+def compact_line(res: dict, detail: str | None = None, limit: int = LINE_LIMIT) -> dict:
+    """The one stdout line (≤ `limit` bytes of JSON): the headline fields,
+    `config`, `roofline` as scalars, `cpu_baseline`, `parity`, the device's
+    bus id, per-rank scalars at N > 1, and every extra leg reduced to its
+    scalars.  Everything else (traces, timelines, sweeps, the nested `valu`
+    block, rank identities) stays in the side file `detail` that bench.py
+    writes beside it.  If the legs still overflow, they are cut down in
+    steps — nested scalars first, then to value/bound/error — and never the
+    headline, roofline, cpu_baseline or parity."""
+    keep = {}
+    for k, v in res.items():
+        if k in LEGS or k in ("roofline", "ranks", "device"):
+            continue
+        keep[k] = v
+    if "roofline" in res:
+        keep["roofline"] = _scalars(res["roofline"], 0)
+    if "device" in res:
+        keep["device"] = {k: res["device"].get(k) for k in ("device_index", "pci_bus_id")}
+    if "ranks" in res:
+        rk = res["ranks"]
+        keep["ranks"] = {k: rk[k] for k in ("step_ms", "kernel_ms", "verdict_gather_ms", "clock_GHz",
+                                             "distinct_devices") if k in rk}
+        keep["ranks"]["pci_bus_ids"] = [d.get("pci_bus_id") for d in rk.get("devices", [])]
+    if detail:
+        keep["detail"] = detail
+    legs = [k for k in LEGS if k in res]
+    for depth in (1, 0, -1):  # -1: value, bound and error only
+        line = dict(keep)
+        for k in legs:
+            v = res[k]
+            if not isinstance(v, dict):
+                line[k] = v
+            elif depth < 0:
+                line[k] = {f: v[f] for f in ("value", "unit") if f in v}
+                if v.get("error"):
+                    line[k]["error"] = str(v["error"])[:240]
+            else:
+                line[k] = _scalars(v, depth)
+        if len(json.dumps(line)) <= limit:
+            return line
+    for k in legs:  # a pathological leg: drop them whole, the headline must print
+        line.pop(k, None)
+    if len(json.dumps(line)) > limit:
+        raise ValueError(f"bench line {len(json.dumps(line))} B over {limit} B without any leg")
+    return line
+
+
 CLOCK_BLOCKS = 256  # stamp workgroups: 32 per XCC under round-robin dispatch
 
 
@@ -1346,6 +1429,9 @@ def main() -> int:
                     help="nccl (= RCCL on ROCm, the real path) or gloo (single-GPU multi-rank rehearsal)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank uses cuda:0 (with --dist-backend gloo)")
+    ap.add_argument("--detail", default=None,
+                    help="side file for the full record (traces, sweeps, identities); default bench_detail.json "
+                         "beside bench.py.  stdout carries only the compact line (compact_line, <= 8 KB)")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -1604,7 +1690,16 @@ def main() -> int:
         if not args.no_reverify and not multi:
             leg(("reverify", "reverify_cold"), reverify_leg)
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        # the full record to the side file, the compact line (≤ 8 KB) to stdout
+        detail = args.detail or os.path.join(ROOT, "bench_detail.json")
+        name = os.path.relpath(detail, ROOT) if detail.startswith(ROOT + os.sep) else detail
+        try:
+            with open(detail, "w") as f:
+                json.dump(res, f, indent=1)
+        except OSError as e:
+            log(f"warning: side file {detail} not written: {e}")
+            name = None
+        print(json.dumps(compact_line(res, name)), flush=True)
     if distributed:
         dist.destroy_process_group()
     return 0

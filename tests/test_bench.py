@@ -35,6 +35,12 @@ def _lines(out: str):
     return [json.loads(x) for x in out.splitlines() if x.startswith("{")]
 
 
+def _check_line_size(out: str):
+    """The result line the driver parses stays within bench.LINE_LIMIT (8 KB)."""
+    (line,) = [x for x in out.splitlines() if x.startswith("{")]
+    assert len(line.encode()) <= 8192, len(line)
+
+
 def test_world_size_must_match_gpus():
     r = _run(["--gpus", "2"] + SMALL, {"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"}, timeout=120)
     assert r.returncode != 0 and not _lines(r.stdout)
@@ -135,23 +141,30 @@ def test_plain_multi_gpu_refused_on_one_gpu_box(built, gpu):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n", [2, 8])
-def test_plain_bench_launches_its_ranks(built, gpu, n):
+def test_plain_bench_launches_its_ranks(built, gpu, n, tmp_path):
     """n = 8 rehearses config 4's shape on the one-GPU box: 8 ranks, global
     piece indices r*1024 + i, the verdicts of all 8 shards gathered and the
     exact 1 % mismatch set checked on the gathered table."""
-    r = _run(["--gpus", str(n), "--same-device", "--dist-backend", "gloo"] + SMALL, timeout=300)
+    side = tmp_path / "detail.json"
+    r = _run(["--gpus", str(n), "--same-device", "--dist-backend", "gloo", "--detail", str(side)] + SMALL,
+             timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     (res,) = _lines(r.stdout)
+    _check_line_size(r.stdout)
+    assert res["detail"] == str(side)
     assert res["n_gpus"] == n and res["world_size"] == n and res["backend"] == "gloo"
     assert res["value"] > 0 and res["config"]["pieces_per_gpu"] == 1024
     assert res["config"]["total_GiB"] == n * 1024 * 256 / (1 << 20)
     rk = res["ranks"]  # every rank's step, kernel and verdict-gather times
     assert all(len(rk[k]) == n for k in ("step_ms", "kernel_ms", "verdict_gather_ms"))
     assert max(rk["step_ms"]) == pytest.approx(res["ms_per_step"], rel=1e-3)
-    # identity: every rank names its device; all share the one GPU here, and the line says so
-    assert [d["rank"] for d in rk["devices"]] == list(range(n))
-    assert all(d["world_size"] == n and d["pci_bus_id"] == rk["devices"][0]["pci_bus_id"] for d in rk["devices"])
-    assert rk["distinct_devices"] is False
+    # identity: every rank names its device (in full in the side file); all share the one GPU here,
+    # and the line says so
+    full = json.loads(side.read_text())
+    devs = full["ranks"]["devices"]
+    assert [d["rank"] for d in devs] == list(range(n)) and rk["pci_bus_ids"] == [d["pci_bus_id"] for d in devs]
+    assert all(d["world_size"] == n and d["pci_bus_id"] == devs[0]["pci_bus_id"] for d in devs)
+    assert rk["distinct_devices"] is False and full["value"] == res["value"]
     assert all(1.0 < g < 3.0 for g in rk["clock_GHz"])
     # every gathered verdict checked, clean pieces against the CPU pool's digests
     assert res["parity"]["checked"] == n * 1024 and res["config"]["parity_checked"] == n * 1024
@@ -161,7 +174,7 @@ def test_plain_bench_launches_its_ranks(built, gpu, n):
 
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
-def test_config4_full_size_8_ranks(built, gpu):
+def test_config4_full_size_8_ranks(built, gpu, tmp_path):
     """BASELINE config 4 at full size on the box's one GPU: 8 gloo ranks x
     65,536 x 256 KiB = 524,288 pieces (128 GiB in one GPU's HBM), global piece
     indices r*65536 + i.  Each rank's expected table is the CPU pool
@@ -170,10 +183,13 @@ def test_config4_full_size_8_ranks(built, gpu):
     gathered table — exactly the 1 % corrupted pieces mismatch — proves all
     519,046 clean digests bit-exact against vortex's pool."""
     args = ["--gpus", "8", "--same-device", "--dist-backend", "gloo", "--pieces", "65536", "--steps", "2",
-            "--warmup", "1", "--no-e2e", "--no-ragged", "--no-reverify", "--no-cpu-baseline"]
+            "--warmup", "1", "--no-e2e", "--no-ragged", "--no-reverify", "--no-cpu-baseline",
+            "--detail", str(tmp_path / "detail.json")]
     r = _run(args, timeout=840)
     assert r.returncode == 0, r.stderr[-3000:]
     (res,) = _lines(r.stdout)
+    _check_line_size(r.stdout)  # the N=8 shape the driver's 8-GPU node prints
+    assert len(res["ranks"]["pci_bus_ids"]) == 8 and res["roofline"]["frac"] > 0
     assert res["n_gpus"] == 8 and res["world_size"] == 8 and res["config"]["pieces_per_gpu"] == 65536
     assert res["config"]["total_GiB"] == 128.0
     p = res["parity"]
@@ -183,21 +199,25 @@ def test_config4_full_size_8_ranks(built, gpu):
 
 
 @pytest.mark.gpu
-def test_bench_rccl_world_size_1(built, gpu):
+def test_bench_rccl_world_size_1(built, gpu, tmp_path):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
-           "--master-addr=127.0.0.1", f"--master-port={port}", BENCH, "--gpus", "1"] + SMALL
+           "--master-addr=127.0.0.1", f"--master-port={port}", BENCH, "--gpus", "1"] + SMALL \
+        + ["--detail", str(tmp_path / "detail.json")]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     (res,) = _lines(r.stdout)
+    _check_line_size(r.stdout)  # the RCCL line prints the compact form too
+    full = json.loads((tmp_path / "detail.json").read_text())
     assert res["n_gpus"] == 1 and res["world_size"] == 1 and res["backend"] == "nccl"
     assert "nccl all-gather of verdicts" in res["config"]["workload"]
     assert len(res["ranks"]["verdict_gather_ms"]) == 1 and res["ranks"]["verdict_gather_ms"][0] > 0
-    assert res["ranks"]["distinct_devices"] is True and res["ranks"]["devices"][0]["world_size"] == 1
-    clk = res["roofline"]["valu"]["clock_run"]
+    assert res["ranks"]["distinct_devices"] is True and full["ranks"]["devices"][0]["world_size"] == 1
+    assert "valu" not in res["roofline"]
+    clk = full["roofline"]["valu"]["clock_run"]
     assert 1.0 < clk["GHz_mean"] < 3.0 and 0 < clk["kernel_busy_frac"] <= 1.0
     frac = clk["one_wave_issue_at_run_clock"]["frac"]  # null when gathers fill > 0.1 of the stamped span
     assert (frac is None) == (clk["kernel_busy_frac"] < 0.9) and (frac is None or frac > 0)
@@ -205,7 +225,7 @@ def test_bench_rccl_world_size_1(built, gpu):
 
 
 @pytest.mark.gpu
-def test_reverify_multi_leg_rccl_world_size_1(built, gpu):
+def test_reverify_multi_leg_rccl_world_size_1(built, gpu, tmp_path):
     """The N>1 config-5 leg on RCCL (verdicts gathered on the device, identity
     and times through nccl's all_gather_object), at the one world size the box
     allows for RCCL: what the driver's 8-GPU run takes, minus the other ranks."""
@@ -214,12 +234,15 @@ def test_reverify_multi_leg_rccl_world_size_1(built, gpu):
         port = s.getsockname()[1]
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     args = ["--pieces", "1024", "--steps", "2", "--warmup", "1", "--no-e2e", "--no-ragged", "--no-cpu-baseline",
-            "--reverify-multi", "--reverify-multi-scale", "0.05"]
+            "--reverify-multi", "--reverify-multi-scale", "0.05", "--detail", str(tmp_path / "detail.json")]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
            "--master-addr=127.0.0.1", f"--master-port={port}", BENCH, "--gpus", "1"] + args
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
-    (res,) = _lines(r.stdout)
+    (line,) = _lines(r.stdout)
+    _check_line_size(r.stdout)
+    res = json.loads((tmp_path / "detail.json").read_text())
+    assert line["reverify_multi"]["warm.value"] == res["reverify_multi"]["warm"]["value"]
     assert res["backend"] == "nccl" and "reverify" not in res
     rm = res["reverify_multi"]
     assert "error" not in rm, rm
@@ -250,7 +273,7 @@ def test_clock_from_stamps():
 
 
 @pytest.mark.gpu
-def test_reverify_multi_leg_rehearsal(built, gpu):
+def test_reverify_multi_leg_rehearsal(built, gpu, tmp_path):
     """The N>1 line's config-5 leg (bench.reverify_multi_leg), rehearsed with 2
     gloo ranks on the box's one GPU and 5 % of linux-mint's pieces: every rank
     verifies its piece range on its GPU, the slowest rank's time is the call's,
@@ -258,10 +281,11 @@ def test_reverify_multi_leg_rehearsal(built, gpu):
     and the CPU pool restatement runs beside it with every host CPU."""
     args = ["--pieces", "1024", "--steps", "2", "--warmup", "1", "--no-e2e", "--no-ragged", "--no-cpu-baseline",
             "--gpus", "2", "--same-device", "--dist-backend", "gloo", "--reverify-multi",
-            "--reverify-multi-scale", "0.05"]
+            "--reverify-multi-scale", "0.05", "--detail", str(tmp_path / "detail.json")]
     r = _run(args, timeout=400)
     assert r.returncode == 0, r.stderr[-3000:]
-    (res,) = _lines(r.stdout)
+    _check_line_size(r.stdout)
+    res = json.loads((tmp_path / "detail.json").read_text())
     rm = res["reverify_multi"]
     assert "error" not in rm, rm
     assert rm["ranks"] == 2 and rm["same_device"] is True and rm["cpu_pool_verdicts_ok"] is True
@@ -376,3 +400,88 @@ def test_roofline_scalars_for_the_record():
     # a span the kernels fill only half of (gathers, N > 1): the mean clock is not theirs
     r2 = bench.roofline(65536, 262144, 4.9, 1.0, "w", dict(clock, span_ms=196.0), steps=20)
     assert r2["clock_kernel_busy_frac"] == pytest.approx(0.5) and r2["valu_issue_frac_run_clock"] is None
+
+
+# The keys the record must carry in the parsed line (VERDICT r5 "Next round" 1).
+ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "traffic_ratio", "kernel_ms",
+             "algorithmic_bytes_per_launch", "clock_GHz_run", "clock_GHz_run_min", "clock_kernel_busy_frac",
+             "valu_Tops", "valu_issue_frac_run_clock", "valu_issue_frac_nominal")
+HEAD_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+             "vs_baseline", "dtype", "data", "config", "roofline", "parity", "cpu_baseline")
+
+
+def _record_line(path):
+    with open(os.path.join(ROOT, path)) as f:
+        return json.loads([x for x in f if x.startswith("{")][-1])
+
+
+def test_compact_line_of_round5_record():
+    """Round 5's 23 KB line (profiles/r05/bench_head.json) through the same
+    compaction bench.py now applies: ≤ 8 KB, every key the record is read
+    for, roofline scalars only, each leg's value, the split's figures."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    full = _record_line("profiles/r05/bench_head.json")
+    assert len(json.dumps(full)) > 20000
+    line = bench.compact_line(full, "bench_detail.json")
+    text = json.dumps(line)
+    assert len(text.encode()) <= 8192
+    for k in HEAD_KEYS:
+        assert k in line, k
+    for k in ROOF_KEYS:
+        assert line["roofline"][k] == full["roofline"][k], k
+    assert not any(isinstance(v, (dict, list)) for v in line["roofline"].values())
+    assert line["cpu_baseline"] == full["cpu_baseline"] and line["parity"] == full["parity"]
+    assert line["value"] == full["value"] and line["config"] == full["config"]
+    for leg in bench.LEGS:
+        if leg in full:
+            assert line[leg]["value"] == full[leg]["value"], leg
+    assert line["reverify"]["split.value"] == full["reverify"]["split"]["value"]
+    assert line["reverify"]["split.best_value"] == full["reverify"]["split"]["best_value"]
+    assert line["reverify_cold"]["disk_direct.value"] == full["reverify_cold"]["disk_direct"]["value"]
+    assert line["reverify"]["cpu_pool.value"] == full["reverify"]["cpu_pool"]["value"]
+    assert "gpu_traces" not in text and "timeline" not in text and line["detail"] == "bench_detail.json"
+
+
+def test_compact_line_of_8_rank_shape():
+    """The N=8 shape (round 4's 8-rank line plus a reverify_multi leg): per-rank
+    lists and bus ids stay, identities go to the side file, ≤ 8 KB."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    full = _record_line("profiles/r04/round_end_head/bench_8rank.json")
+    assert len(full["ranks"]["devices"]) == 8
+    full["reverify_multi"] = {"warm": {"value": 150.0, "rank_traces": [[{"wall_ms": 1.0}] * 8] * 5,
+                                       "cpu_pool": {"value": 30.0}},
+                              "cold": {"value": 40.0}, "ranks": 8, "pieces": 1387,
+                              "split": {"value": 160.0, "s_runs": [0.02] * 7, "sample": "x" * 400}}
+    line = bench.compact_line(full, "bench_detail.json")
+    assert len(json.dumps(line).encode()) <= 8192
+    rk = line["ranks"]
+    assert len(rk["step_ms"]) == 8 and len(rk["pci_bus_ids"]) == 8 and "devices" not in rk
+    assert line["reverify_multi"]["warm.value"] == 150.0 and line["reverify_multi"]["split.value"] == 160.0
+    for k in ("metric", "value", "n_gpus", "roofline", "config"):  # (round 4's line had no `parity` yet)
+        assert k in line
+
+
+def test_compact_line_never_drops_the_headline():
+    """Legs that stay too large even as scalars are cut down, in steps, to
+    value/error and then away; the headline, roofline, cpu_baseline and
+    parity always print."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    full = _record_line("profiles/r05/bench_head.json")
+    big = {f"k{i}": float(i) for i in range(400)}
+    for leg in ("ragged", "e2e", "reverify"):
+        full[leg] = dict(big, value=1.5, error=None)
+    line = bench.compact_line(full, None)
+    assert len(json.dumps(line).encode()) <= 8192
+    assert line["ragged"] == {"value": 1.5} and "detail" not in line
+    full["e2e_async"] = {"error": "E" * 5000}
+    line = bench.compact_line(full, None)
+    assert len(line["e2e_async"]["error"]) == 240
+    full["ragged"] = {"value": 1.0, "unit": "u" * 9000}
+    line = bench.compact_line(full, None)
+    assert "ragged" not in line and all(k in line for k in HEAD_KEYS)
