@@ -163,8 +163,13 @@ int vx_unregister_host_buffer(vx_ctx* ctx, void* ptr);
  *               batch launch failed part way, the device may still read
  *               `data` until vx_destroy returns.
  *   VX_EBUSY    (only with vx_config.refuse_when_full = 1) every slot is in
- *               flight and the open batch is full: nothing waited, the
- *               context is unchanged; hash the piece on the caller's pool.
+ *               flight and the open batch is full: the piece was NOT taken
+ *               and nothing waited; hash it on the caller's pool.  Before
+ *               refusing, the call may have launched the full open batch (the
+ *               launch the next submit makes anyway; stats.batches + 1) and
+ *               harvested finished batches without blocking (their results
+ *               wait for vx_poll).  No piece changes owner: vx_pending() is
+ *               the same before and after a refused call.
  * (VX_ENODEV is not returned by submits.) */
 int vx_submit(vx_ctx* ctx, uint64_t tag, const uint8_t* data, uint32_t len, const uint8_t* expected);
 /* Device-resident expected-digest table: upload the
@@ -174,7 +179,9 @@ int vx_submit(vx_ctx* ctx, uint64_t tag, const uint8_t* data, uint32_t len, cons
  * table; requires no pieces in flight. */
 int vx_set_piece_table(vx_ctx* ctx, const uint8_t* table, uint32_t n_pieces);
 /* vx_submit with expected = row piece_index of the piece table (same
- * ownership rule and return codes). */
+ * ownership rule and return codes, VX_EBUSY under refuse_when_full included:
+ * the full open batch may be launched and finished batches harvested before
+ * the refusal, the refused piece is not taken). */
 int vx_submit_piece(vx_ctx* ctx, uint64_t tag, const uint8_t* data, uint32_t len, uint32_t piece_index);
 /* Launch whatever is queued (call once per event-loop turn, next to the
  * drain at event_loop.rs:554-557).  If launching would leave no batch slot

@@ -308,12 +308,14 @@ def test_submit_ownership_every_tag_once(built, gpu, mode):
 
 def test_refuse_when_full_never_blocks(built, gpu):
     """vx_config.refuse_when_full = 1 (ABI 3): when every slot is in flight
-    and the open batch is full, vx_submit returns VX_EBUSY at once — the
-    piece not taken, the context unchanged — instead of waiting for the
-    oldest batch, so the event loop hands the piece to its own pool.  Every
-    piece is verified exactly once, on whichever side took it; the engine
-    never stalls the submitting thread (submit_stall_ns == 0) and counts
-    its refusals."""
+    and the open batch is full, vx_submit returns VX_EBUSY at once instead of
+    waiting for the oldest batch, so the event loop hands the piece to its
+    own pool.  The documented invariant (vx_hash.h VX_EBUSY): the refused
+    piece is not taken, vx_pending() is unchanged, and the only launch a
+    refusal may make is the full open batch's (batches + 1, and then only
+    when that batch held batch_pieces pieces).  Every piece is verified
+    exactly once, on whichever side took it; the engine never stalls the
+    submitting thread (submit_stall_ns == 0) and counts its refusals."""
     from vortex_amd._lib import VX_EBUSY, VxError
     from vortex_amd.hash_pool import HashPool
 
@@ -326,14 +328,26 @@ def test_refuse_when_full_never_blocks(built, gpu):
     verdict_truth = [hashlib.sha1(bytes(b)).digest() == w for b, w in zip(bufs, want)]
     # 2 slots of 8 pieces: 16 pieces fill the pipeline, and 1 MiB chains keep it full for a while
     with HashPool(plen, slots=2, batch_pieces=8, slot_bytes=8 << 20, refuse_when_full=1) as pool:
-        got, refused = {}, []
+        got, refused, launched_on_refusal = {}, [], 0
+        taken = 0  # pieces the engine took; every launch before a refusal holds exactly 8
         for i in range(n):
+            pend, batches = pool.pending, pool.stats()["batches"]
             try:
                 pool.spawn(i, 7, bufs[i], plen, want[i])
+                taken += 1
             except VxError as e:
                 assert e.code == VX_EBUSY and e.refused[0] == i and e.refused[2] is bufs[i]
                 refused.append(i)  # vortex's own pool hashes it (here: hashlib)
                 got[i] = hashlib.sha1(bytes(bufs[i])).digest() == want[i]
+                # the invariant: no piece changed owner; at most the full open batch launched
+                assert pool.pending == pend
+                delta = pool.stats()["batches"] - batches
+                assert delta in (0, 1)
+                if delta:
+                    assert taken == 8 * (batches + 1), (taken, batches)  # the open batch was full
+                    launched_on_refusal += 1
+                else:
+                    assert taken == 8 * batches  # nothing open was left unlaunched
         assert refused, "the pipeline never filled: no refusal to test"
         pool.drain()
         for r in pool.try_iter():
@@ -349,3 +363,37 @@ def test_refuse_when_full_never_blocks(built, gpu):
         pool.drain()
         (r,) = pool.try_iter()
         assert r.hash_matched
+
+
+@pytest.mark.parametrize("copy_stream", [1, 0])
+def test_chunk_round_failure_then_reuse_and_destroy(built, gpu, tmp_path, copy_stream):
+    """A re-verify whose k-th chunk round fails after its data copy was
+    queued (injected: vx_tuning_fail_launch_after, between the copy and the
+    kernel launch), on the copy stream (verify_copy_stream = 1, the default)
+    and on the slot streams (0).  The call returns the error only after the
+    queued part of the round finished (a stale `done` event must
+    not free a slot under a DMA); the same context's next call is bit-exact
+    against the oracle on a file with a damaged piece; vx_destroy then waits
+    for the copy stream before it frees the stages."""
+    from vortex_amd._lib import VX_EDEVICE, VxError
+    from vortex_amd.hash_pool import HashPool
+
+    pl, n = 2 << 20, 24
+    path = tmp_path / "t.bin"
+    path.write_bytes(b"".join(oracle.gen_piece(0xC5, i, pl) for i in range(n)))
+    exp = b"".join(oracle.sha1(oracle.gen_piece(0xC5, i, pl)) for i in range(n))
+    with open(path, "r+b") as f:  # piece 9 damaged on disk
+        f.seek(9 * pl + 12345)
+        f.write(b"\x00\xff")
+    want = oracle.pool_verify_files([str(path)], [n * pl], pl, exp, threads=4)
+    assert sum(want) == n - 1
+    for fail_at in (0, 5, 17):
+        with HashPool(pl, slots=3, slot_bytes=8 << 20, verify_chunk=65536, hooks=True) as pool:
+            pool.lib.vx_tuning_verify_copy_stream(pool._h, copy_stream)
+            pool.lib.vx_tuning_fail_launch_after(pool._h, fail_at)
+            with pytest.raises(VxError) as ei:
+                pool.verify_files([str(path)], [n * pl], pl, exp, io_threads=4)
+            assert ei.value.code == VX_EDEVICE and "injected" in str(ei.value)
+            got, bad = pool.verify_files([str(path)], [n * pl], pl, exp, io_threads=4)
+            assert got == want and bad == 0
+            assert pool.stats()["chunk_rounds"] > fail_at

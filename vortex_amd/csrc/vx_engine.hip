@@ -278,6 +278,10 @@ uint8_t* alloc_stage(uint64_t bytes, bool huge, uint64_t* mapped) {
     if (r + len + kHuge > a + len) munmap(reinterpret_cast<void*>(a + len), r + len + kHuge - (a + len));
     uint8_t* p = reinterpret_cast<uint8_t*>(a);
     (void)madvise(p, len, MADV_HUGEPAGE);  // a hint: 4 KiB pages where THP is off
+    // A client that forks (hooks, helpers) must not turn the pinned pages
+    // copy-on-write in the parent: the GPU keeps DMAing to the pinned page
+    // while a write after the fork would move the parent to a new one.
+    (void)madvise(p, len, MADV_DONTFORK);
     for (uint64_t o = 0; o < len; o += 4096) p[o] = 0;
     if (hipHostRegister(p, len, hipHostRegisterDefault) != hipSuccess) {
         munmap(p, len);
@@ -908,6 +912,9 @@ int vx_destroy(vx_ctx* c) {
     // return in-flight buffers to its pool as soon as this call returns.
     for (auto& s : c->slots)
         if (s.stream) (void)hipStreamSynchronize(s.stream);
+    // the re-verify's data copies run on the copy stream: a failed call may
+    // have left one queued that still reads a stage or writes an arena
+    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);
     for (auto& r : c->registered) (void)hipHostUnregister(reinterpret_cast<void*>(r.first));
     for (auto& s : c->slots) free_slot_mem(s);
     if (c->d_table) (void)hipFree(c->d_table);
@@ -916,10 +923,7 @@ int vx_destroy(vx_ctx* c) {
     for (hipEvent_t e : c->copy_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->anchor_ev) (void)hipEventDestroy(c->anchor_ev);
-    if (c->copy_stream) {
-        (void)hipStreamSynchronize(c->copy_stream);
-        (void)hipStreamDestroy(c->copy_stream);
-    }
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     delete c;
     return rc;
 }
@@ -1348,6 +1352,10 @@ struct ChunkPipe {
         mark_launched(c, si);
         if (!rc && continues && have_prev && hipStreamWaitEvent(st, prev_kernel, 0) != hipSuccess)
             rc = fail(VX_EDEVICE, "chunk round: stream wait failed");
+#ifdef VX_TEST_HOOKS
+        if (!rc && c->fail_launch_after >= 0 && c->fail_launch_after-- == 0)
+            rc = fail(VX_EDEVICE, "chunk round: injected launch failure (vx_tuning_fail_launch_after)");
+#endif
         if (!rc) {
             hipError_t e = vx::launch_chunk(s.d_arena, s.d_offsets, s.d_lens, m, s.d_pidx, s.d_poff, s.d_tlen,
                                             d_states, d_dig, d_exp, d_match, st);
@@ -1360,6 +1368,7 @@ struct ChunkPipe {
         s.state = Slot::INFLIGHT;
         s.seq = c->seq++;
         s.n = 0;  // nothing to harvest: outputs live in the call's device rows
+        if (rc) (void)hipStreamSynchronize(st);  // s.done may be stale: let the queued part finish
         if (!rc) rc = reap(c, false);
         return rc;
     }
@@ -1389,6 +1398,10 @@ struct ChunkPipe {
             rc = fail(VX_EDEVICE, "chunk round: stream wait failed");
         if (!rc && continues && have_prev && hipStreamWaitEvent(st, prev_kernel, 0) != hipSuccess)
             rc = fail(VX_EDEVICE, "chunk round: stream wait failed");
+#ifdef VX_TEST_HOOKS
+        if (!rc && c->fail_launch_after >= 0 && c->fail_launch_after-- == 0)
+            rc = fail(VX_EDEVICE, "chunk round: injected launch failure (vx_tuning_fail_launch_after)");
+#endif
         if (!rc) {
             hipError_t e = vx::launch_chunk(s.d_arena, s.d_offsets, s.d_lens, m, s.d_pidx, s.d_poff, s.d_tlen,
                                             d_states, d_dig, d_exp, d_match, st);
@@ -1401,6 +1414,14 @@ struct ChunkPipe {
         s.state = Slot::INFLIGHT;
         s.seq = c->seq++;
         s.n = 0;
+        if (rc) {
+            // Part of the round may be queued (its data copy on the copy
+            // stream, the table on the slot's) while s.done was not recorded
+            // for it: wait for both here, so no later reuse or free of the
+            // stage and arena races a DMA of this round.
+            (void)hipStreamSynchronize(cs);
+            (void)hipStreamSynchronize(st);
+        }
         if (!rc) rc = reap(c, false);
         return rc;
     }
@@ -1437,6 +1458,7 @@ struct ChunkPipe {
     // The rows and the event belong to the context (freed by vx_destroy);
     // only make sure nothing of this call is still running.
     void release() {
+        if (cs) (void)hipStreamSynchronize(cs);  // data copies of this call's rounds
         for (auto& s : c->slots)
             if (s.stream) (void)hipStreamSynchronize(s.stream);
     }
@@ -2316,6 +2338,7 @@ void vx_tuning_verify_copy_stream(vx_ctx* c, int mode) {
 void vx_tuning_stage_huge(vx_ctx* c, int on) {
     if (!c) return;
     c->stage_huge = on ? 1 : 0;
+    if (c->copy_stream) (void)hipStreamSynchronize(c->copy_stream);  // no copy still reads a stage
     for (auto& s : c->slots)  // reallocated on next use (every slot is idle between calls)
         if (s.state == Slot::FREE) free_stage(s);
 }
