@@ -626,6 +626,53 @@ def split_call(pool, paths: list, lens: list, n: int, pl: int, exp: bytes, first
             "matched": merged}
 
 
+def balanced_call(pool, paths: list, lens: list, n: int, pl: int, exp: bytes, io_threads: int, cpu_threads: int,
+                  cpu_thread_rate: float) -> dict:
+    """One bulk re-verify shared by the engine and vortex's pool with no plan
+    (vx_verify_files_split, INTEGRATION.md "The split"): the pool stand-in
+    (oracle/pool_oracle.cpp's claim pool, kind "port": vortex's rayon threads
+    calling vx_split_claim) takes pieces from the head while the engine takes
+    groups from the top, sized from both sides' rates as measured in the call.
+    Returns wall time, each side's time, the boundary, and the verdicts."""
+    import threading
+
+    import oracle
+    from vortex_amd.hash_pool import Split
+
+    sp = Split(0, n, cpu_threads, cpu_thread_rate)
+    res, errs = {}, []
+
+    def gpu():
+        try:
+            t0 = time.perf_counter()
+            res["gpu_bad"] = pool.verify_files_split(paths, lens, pl, exp, sp, io_threads=io_threads)
+            res["gpu_s"] = time.perf_counter() - t0
+        except Exception as e:  # noqa: BLE001  (raised below, on the calling thread)
+            errs.append(e)
+
+    def cpu():
+        try:
+            t0 = time.perf_counter()
+            res["taken"] = oracle.pool_verify_files_claim(paths, lens, pl, exp, cpu_threads, sp.claim_fn, sp.done_fn,
+                                                          sp.arg, 0, sp.matched)
+            res["cpu_s"] = time.perf_counter() - t0
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=gpu), threading.Thread(target=cpu)]
+    t0 = time.perf_counter()
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    wall = time.perf_counter() - t0
+    if errs:
+        raise errs[0]
+    got = sp.verdicts()
+    return {"s": wall, "gpu_s": res["gpu_s"], "cpu_s": res["cpu_s"], "ok": all(got) and res["gpu_bad"] == 0,
+            "boundary": sp.boundary, "pool_pieces": res["taken"], "matched": got}
+
+
 def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
     """BASELINE config 5: full re-verify of a torrent's data from disk with
     the linux-mint geometry (cli/linux-mint.torrent: 2,907,832,320 B, 2 MiB
@@ -718,9 +765,18 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
             # alone (all threads) as references, so a box's drift lands on all of them alike.
             cfgs = [(first, io_t, pool_t) for first in points] + [(0, threads, threads), (n, threads, threads)]
             by_cfg = {c: [] for c in cfgs}
+            bal = []  # the self-balancing split (no plan), in the same alternation
             for _ in range(split_reps):
                 for c in cfgs:
                     by_cfg[c].append(split_call(pool, [path], [total], n, pl, exp, c[0], c[1], c[2]))
+                bal.append(balanced_call(pool, [path], [total], n, pl, exp, io_t, pool_t, rate))
+            assert all(b["ok"] for b in bal), "balanced split: a verdict differs from the expected table"
+            bm = sorted(bal, key=lambda b: b["s"])[len(bal) // 2]
+            split["balanced"] = {"io_threads": io_t, "cpu_threads": pool_t, "value": round(total / bm["s"] / GiB, 2),
+                                 "s_runs": [round(b["s"], 4) for b in bal],
+                                 "gpu_first_runs": [b["boundary"] for b in bal],
+                                 "gpu_s": round(bm["gpu_s"], 4), "cpu_s": round(bm["cpu_s"], 4),
+                                 "gpu_first": bm["boundary"]}
             for (first, io_c, pool_c), calls in by_cfg.items():
                 assert all(c["ok"] for c in calls), "split re-verify: a verdict differs from the expected table"
                 med = sorted(calls, key=lambda c: c["s"])[len(calls) // 2]
@@ -779,23 +835,30 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
     warm, cold = record("warm"), record("cold")
     best = max(split["configs"], key=lambda c: c["value"])
     planned = [c for c in split["configs"] if c["planned"]]
-    # `value` is the planner's point: what a caller following vx_plan_verify_split
-    # gets; the best of the three points stays beside it (how far the plan is off)
+    # `value` is the self-balancing split's (vx_verify_files_split: no plan, the
+    # boundary found at run time); the planner's point and the best of the three
+    # fixed points stay beside it, so the record shows how far either is off
     pv = max(c["value"] for c in planned) if planned else best["value"]
+    bv = split["balanced"]["value"]
     either = max(split["gpu_alone"]["value"], split["pool_alone"]["value"], warm["value"], warm["cpu_pool"]["value"])
-    split.update({"value": pv, "unit": "GiB/s", "planned": bool(planned),
+    split.update({"value": bv, "unit": "GiB/s", "kind": "balanced (vx_verify_files_split)",
+                  "balanced_vs_best_fixed": round(bv / best["value"], 4),
+                  "planned_value": pv, "planned_vs_best_fixed": round(pv / best["value"], 4),
                   "best_value": best["value"], "best_gpu_first": best["gpu_first"],
-                  "best_io_threads": best["io_threads"],
+                  "best_io_threads": best["io_threads"], "balanced_gpu_first": split["balanced"]["gpu_first"],
                   "gpu_only": split["gpu_alone"]["value"], "pool_only": split["pool_alone"]["value"],
                   # against the better of each side's two figures: in the alternation and in the legs above
-                  "beats_both": pv > either, "best_beats_both": best["value"] > either,
+                  "beats_both": bv > either, "planned_beats_both": pv > either,
+                  "best_beats_both": best["value"] > either,
                   "pool_kind": "port",
-                  "sample": f"the warm file split at GPU pieces [first, {n}) via vx_verify_files_range while the CPU "
-                            f"pool restatement (vortex's par_iter stand-in, 3/4 of the {threads} threads) verifies "
-                            f"[0, first) at once; first = vx_plan_verify_split's {split['plan']['gpu_first']} and the "
-                            f"points with 10 % fewer / more GPU pieces, engine readers at half the threads; "
-                            f"alternating call by call with the GPU alone and the pool alone (gpu_only / "
-                            f"pool_only); median of {split_reps} per config; every verdict checked"})
+                  "sample": f"the warm file shared by the engine and the CPU pool restatement (vortex's par_iter "
+                            f"stand-in, 3/4 of the {threads} threads) at once: balanced = vx_verify_files_split "
+                            f"(the pool claims from the head, the engine sizes its groups from the rates it "
+                            f"measures); fixed points = vx_verify_files_range over [first, {n}) with the pool on "
+                            f"[0, first), first = vx_plan_verify_split's {split['plan']['gpu_first']} and 10 % "
+                            f"fewer / more GPU pieces; engine readers at half the threads; alternating call by "
+                            f"call with the GPU alone and the pool alone (gpu_only / pool_only); median of "
+                            f"{split_reps} per config; every verdict checked"})
     warm["split"] = split
     where = {"dir": d, "fs": fs_type(d)}
     warm.update({"write_s": round(t_write, 2), "file": where,

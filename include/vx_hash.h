@@ -317,6 +317,55 @@ int64_t vx_verify_files(vx_ctx* ctx, const char* const* paths, const uint64_t* f
 int64_t vx_verify_files_range(vx_ctx* ctx, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
                               uint32_t piece_length, const uint8_t* expected, size_t n_pieces, size_t first,
                               size_t count, uint8_t* matched_out, uint32_t io_threads);
+/* ---- the self-balancing split (round 6) ---------------
+ * One bulk re-verify shared at once by the engine and the caller's own pool
+ * with no plan: torrent.rs:724-740's par_iter balances by rayon work
+ * stealing, and this does the same across the PCIe boundary.  A vx_split is
+ * one claim word over pieces [first, end): the pool takes pieces one by one
+ * from the head (vx_split_claim, one compare-and-swap each), the engine takes
+ * whole groups from the top as it forms its chunk rounds, and the two meet
+ * wherever the host at hand puts them.  Before every round the engine
+ * compares its remaining time with the pool's, both from rates measured in
+ * this call (the pool's finished pieces per second through vx_split_done;
+ * its own copy, read and per-block chain rates from the rounds' GPU events),
+ * and takes the group of pieces that keeps the two finish times equal.
+ * Until the first measurements exist it starts on half of what the cold-start
+ * rates (cpu_threads x cpu_thread_rate, the PCIe rate) would give it, since a
+ * claim cannot be handed back.  The caller owns the struct; it may live on
+ * the stack of the thread that starts both sides. */
+typedef struct vx_split {
+    uint64_t word;          /* head (low 32 bits) | stop (high 32): [head, stop) is unclaimed          */
+    uint64_t pool_done;     /* pieces the pool finished (vx_split_done)                                */
+    uint64_t start_ns;      /* steady clock at vx_split_init: the pool's rate is measured from here     */
+    uint64_t first, end;    /* the range                                                               */
+    uint32_t cpu_threads;   /* the pool's threads (0 = no pool: the engine takes every piece)          */
+    uint32_t _pad;
+    double cpu_thread_rate; /* the pool's bytes/s per thread alone (cold start only; 0 = 2.2e9, SHA-NI) */
+} vx_split;
+/* Pieces [first, end) unclaimed; end - first < 2^32 and end < 2^32. */
+int vx_split_init(vx_split* s, uint64_t first, uint64_t end, uint32_t cpu_threads, double cpu_thread_rate);
+/* Pool side, from any number of threads: the next piece from the head, or -1
+ * when no piece is left for the pool.  After a piece's verdict is written,
+ * call vx_split_done(s, 1): the engine reads the pool's rate from it. */
+int64_t vx_split_claim(vx_split* s);
+void vx_split_done(vx_split* s, uint64_t pieces);
+/* The lowest piece the engine took (end when it took none): once both sides
+ * have returned, the pool verified [first, boundary) and the engine
+ * [boundary, end). */
+uint64_t vx_split_boundary(const vx_split* s);
+/* The engine's side: verifies the pieces it claims from s (always the top of
+ * the range, contiguous) with resumable chunk rounds, while the caller's pool
+ * runs vx_split_claim on its own threads; returns when its pieces are done,
+ * possibly while the pool still works.  matched_out has end - first bytes
+ * (matched_out[k] for piece first + k); the engine writes only its own
+ * pieces' entries, the pool writes the others.  Returns the number of the
+ * engine's pieces that hit an I/O error (>= 0), or a VX_E* code: then the
+ * pieces [vx_split_boundary(s), end) have no verdict and the caller verifies
+ * them itself.  Requires no async pieces pending on ctx.  vx_last_verify and
+ * vx_last_verify_rounds describe the call as for vx_verify_files. */
+int64_t vx_verify_files_split(vx_ctx* ctx, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
+                              uint32_t piece_length, const uint8_t* expected, size_t n_pieces, vx_split* s,
+                              uint8_t* matched_out, uint32_t io_threads);
 /* In-process multi-GPU re-verify: vortex is one process with one event loop
  * (event_loop.rs:385), so on a multi-GPU host it holds one context per GPU
  * (vx_config.device) and hands them all to this call, which replaces the

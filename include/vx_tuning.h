@@ -26,6 +26,7 @@ int vx_sha1_device_ragged_variant(const void* d_base, const uint64_t* d_offsets,
                                   const uint32_t* d_order, uint32_t n, void* d_digests, const void* d_expected,
                                   void* d_matched, void* stream, int variant);
 struct vx_ctx;
+struct vx_split;
 /* How a context with zero_copy = 1 hashes a slot of n registered, aligned
  * pieces of total_len bytes: 1 the zero-copy pair, 2 the zero-copy kernel
  * with a loader wave (n < 128, a latency-bound batch); 0 (gather + hash) is
@@ -65,6 +66,18 @@ int vx_tuning_plan_ragged(uint32_t n, uint32_t max_len, uint64_t total_len);
  * C/4).  Writes up to max (offset, length) pairs to out
  * (2*max uint64_t) and returns the number of rounds (host-only). */
 size_t vx_tuning_chunk_schedule(uint64_t L, uint64_t C, int head, int tail, uint64_t* out, size_t max);
+/* The engine's side of the split's claim word (vx_verify_files_split):
+ * take up to k pieces from the top of the unclaimed range; returns the new
+ * stop, so the engine's pieces are [returned, previous stop) (host-only). */
+uint64_t vx_tuning_split_take_tail(struct vx_split* s, uint64_t k);
+/* The last vx_verify_files_split call's decisions, one row of 12 doubles per
+ * round it formed: ms since the call's start, the pool's rate (pieces/s), the
+ * engine's intake rate (B/s), its chain per 64-byte block (ns), the predicted
+ * remaining ms of the engine and of the pool with the group taken, unclaimed
+ * pieces, the group taken, active lanes, the pool's finished pieces, the
+ * decision mode (0 later round, 1 first, 2 forced) and whether both sides'
+ * rates were measured.  Writes up to max rows; returns the row count. */
+size_t vx_tuning_last_split(const struct vx_ctx* ctx, double* out, size_t max);
 
 int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,
                                    const void* d_expected, void* d_matched, void* stream, int variant);

@@ -65,6 +65,10 @@ def lib() -> ctypes.CDLL:
                                             ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                             ctypes.c_void_p]
         L.vxo_pool_verify_files.restype = ctypes.c_int
+        L.vxo_pool_verify_files_claim.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32,
+                                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+        L.vxo_pool_verify_files_claim.restype = ctypes.c_int64
         L.vxo_sha1_ctx_size.restype = ctypes.c_size_t
         L.vxo_sha1_init.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.vxo_sha1_update.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
@@ -160,6 +164,21 @@ def pool_verify_files(paths, file_lengths, piece_length: int, expected: bytes, t
     out = ctypes.create_string_buffer(max(1, n))
     lib().vxo_pool_verify_files(arr, lens, len(paths), piece_length, exp, n, threads, backend, out)
     return [bool(b) for b in out.raw[:n]]
+
+
+def pool_verify_files_claim(paths, file_lengths, piece_length: int, expected: bytes, threads: int, claim_fn: int,
+                            done_fn: int, arg: int, base: int, out, backend: int = 0) -> int:
+    """The pool beside the engine's split (vx_verify_files_split): `threads`
+    threads take pieces from claim_fn(arg) until it returns -1 — vortex's
+    rayon threads calling vx_split_claim — verify each as
+    check_piece_hash_sync does, write out[i - base] and call done_fn(arg, 1).
+    claim_fn / done_fn / arg are C addresses (the engine's vx_split_claim /
+    vx_split_done and its vx_split).  Returns the pieces the pool took."""
+    arr = (ctypes.c_char_p * max(1, len(paths)))(*[p.encode() for p in paths])
+    lens = (ctypes.c_uint64 * max(1, len(file_lengths)))(*file_lengths)
+    exp = ctypes.create_string_buffer(expected, max(1, len(expected)))
+    return lib().vxo_pool_verify_files_claim(arr, lens, len(paths), piece_length, exp, threads, backend, claim_fn,
+                                             done_fn, arg, base, out)
 
 
 # ---------------------------------------------------------------- geometry

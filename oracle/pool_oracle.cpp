@@ -166,8 +166,45 @@ void vxo_sha1_init(void* c, int backend);
 void vxo_sha1_update(void* c, const uint8_t* p, size_t n);
 void vxo_sha1_final(void* c, uint8_t out[20]);
 
+namespace {
+// The pool's claim source: piece indices from a counter over [0, n) (the
+// plain par_iter), or from a caller's claim function (the split,
+// include/vx_hash.h vx_split_claim / vx_split_done: vortex's rayon threads
+// asking the engine's claim word for the next piece).
+struct Claims {
+    int64_t (*claim)(void*) = nullptr;
+    void (*done)(void*, uint64_t) = nullptr;
+    void* arg = nullptr;
+    uint64_t base = 0;  // matched_out[i - base]
+};
+int pool_verify_files_impl(const char* const* paths, const uint64_t* lens, size_t nfiles, uint32_t piece_length,
+                           const uint8_t* expected, size_t n, int threads, int backend, uint8_t* matched_out,
+                           const Claims* cl);
+}  // namespace
+
 int vxo_pool_verify_files(const char* const* paths, const uint64_t* lens, size_t nfiles, uint32_t piece_length,
                           const uint8_t* expected, size_t n, int threads, int backend, uint8_t* matched_out) {
+    return pool_verify_files_impl(paths, lens, nfiles, piece_length, expected, n, threads, backend, matched_out,
+                                  nullptr);
+}
+
+// The same check_piece_hash_sync per piece, on `threads` threads that take
+// their pieces from claim(arg) until it returns -1, write matched_out[i -
+// base] and call done(arg, 1) after each verdict.  Returns the pieces taken.
+int64_t vxo_pool_verify_files_claim(const char* const* paths, const uint64_t* lens, size_t nfiles,
+                                    uint32_t piece_length, const uint8_t* expected, int threads, int backend,
+                                    int64_t (*claim)(void*), void (*done)(void*, uint64_t), void* arg, uint64_t base,
+                                    uint8_t* matched_out) {
+    if (!claim) return -1;
+    Claims cl{claim, done, arg, base};
+    return pool_verify_files_impl(paths, lens, nfiles, piece_length, expected, 0, threads, backend, matched_out, &cl);
+}
+}  // extern "C"
+
+namespace {
+int pool_verify_files_impl(const char* const* paths, const uint64_t* lens, size_t nfiles, uint32_t piece_length,
+                           const uint8_t* expected, size_t n, int threads, int backend, uint8_t* matched_out,
+                           const Claims* cl) {
     struct Span { int64_t sp, so, ep, eo, len; };
     std::vector<Span> fs;
     int64_t sp = 0, so = 0;
@@ -208,13 +245,32 @@ int vxo_pool_verify_files(const char* const* paths, const uint64_t* lens, size_t
         }
         vxo_sha1_final(ctx.data(), p.digest);
         p.hash_matched = ok && std::memcmp(p.digest, expected + 20 * idx, 20) == 0;
-        result[idx] = p.hash_matched ? 1 : 0;
+        if (cl)
+            matched_out[idx - cl->base] = p.hash_matched ? 1 : 0;  // claimed pieces: written in place
+        else
+            result[idx] = p.hash_matched ? 1 : 0;
         return p;
     };
-    run_pool(n, threads, job, ch);
+    int64_t taken = 0;
+    if (cl) {
+        std::atomic<int64_t> count{0};
+        std::vector<std::thread> ws;
+        for (int t = 0; t < std::max(1, threads); ++t)
+            ws.emplace_back([&] {
+                for (int64_t i; (i = cl->claim(cl->arg)) >= 0;) {
+                    (void)job((size_t)i);
+                    if (cl->done) cl->done(cl->arg, 1);
+                    count.fetch_add(1, std::memory_order_relaxed);
+                }
+            });
+        for (auto& w : ws) w.join();
+        taken = count.load();
+    } else {
+        run_pool(n, threads, job, ch);
+        std::memcpy(matched_out, result.data(), n);
+    }
     for (int fd : fds)
         if (fd >= 0) close(fd);
-    std::memcpy(matched_out, result.data(), n);
-    return 0;
+    return taken;
 }
-}  // extern "C"
+}  // namespace

@@ -1,0 +1,147 @@
+"""GPU: the self-balancing split re-verify (vx_verify_files_split).
+
+The engine and the caller's pool verify one torrent at once with no plan:
+the pool (oracle/pool_oracle.cpp's claim pool, the stand-in for vortex's
+rayon threads calling vx_split_claim) takes pieces from the head, the engine
+takes groups from the top sized from rates it measures during the call.  The
+bar is the reference's own: every verdict equals check_piece_hash_sync's
+(torrent.rs:724-740 over file_store.rs:228-303) on the same files —
+damaged pieces on either side, truncated files (``Err(_) => false``), file
+boundaries inside pieces, pieces shorter and longer than a chunk, ranges that
+start mid-torrent, pools of any size (none at all included) — and every piece
+is verified by exactly one side.
+"""
+import os
+import random
+import threading
+
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _files(tmp_path, pl, sizes, seed):
+    paths = []
+    for k, L in enumerate(sizes):
+        p = tmp_path / f"s{seed}_{k}.bin"
+        p.write_bytes(oracle.gen_piece(seed, k, L))
+        paths.append(str(p))
+    data = b"".join(open(p, "rb").read() for p in paths)
+    exp = b"".join(oracle.sha1(data[i:i + pl]) for i in range(0, len(data), pl))
+    return paths, sizes, exp
+
+
+def _run_split(pool, paths, lens, pl, exp, first, end, cpu_threads, rate=0.0, io_threads=4):
+    from vortex_amd.hash_pool import Split
+
+    sp = Split(first, end, cpu_threads, rate)
+    out = {}
+
+    def engine():
+        try:
+            out["bad"] = pool.verify_files_split(paths, lens, pl, exp, sp, io_threads=io_threads)
+        except Exception as e:  # noqa: BLE001
+            out["err"] = e
+
+    th = threading.Thread(target=engine)
+    th.start()
+    taken = 0
+    if cpu_threads:
+        taken = oracle.pool_verify_files_claim(paths, lens, pl, exp, cpu_threads, sp.claim_fn, sp.done_fn, sp.arg,
+                                               first, sp.matched)
+    th.join()
+    if "err" in out:
+        raise out["err"]
+    return sp, taken, out["bad"]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_split_matches_pool_on_damaged_layouts(built, gpu, tmp_path, seed):
+    from vortex_amd.hash_pool import HashPool
+
+    rng = random.Random(seed)
+    pl = rng.choice([65536, 262144 + 4096, 1 << 20, 2 << 20])
+    nfiles = rng.randint(1, 4)
+    sizes = [rng.randint(0, 40) * pl + rng.randint(0, pl - 1) for _ in range(nfiles)]
+    if sum(sizes) == 0:
+        sizes[0] = 3 * pl + 1
+    paths, sizes, exp = _files(tmp_path, pl, sizes, seed)
+    n = len(exp) // 20
+    total = sum(sizes)
+    for _ in range(rng.randint(1, 4)):  # damaged bytes anywhere (either side)
+        off = rng.randrange(total)
+        acc = 0
+        for p, L in zip(paths, sizes):
+            if off < acc + L:
+                with open(p, "r+b") as f:
+                    f.seek(off - acc)
+                    b = f.read(1)
+                    f.seek(off - acc)
+                    f.write(bytes([b[0] ^ 0x5A]))
+                break
+            acc += L
+    if rng.random() < 0.5:  # a truncated file: its pieces are I/O errors on whichever side
+        k = rng.randrange(nfiles)
+        os.truncate(paths[k], sizes[k] // 2)
+    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
+    first = rng.randint(0, n // 3)
+    end = n - rng.randint(0, n // 4)
+    cpu_threads = rng.choice([0, 1, 3, 8])
+    with HashPool(pl, slots=3, slot_bytes=max(16 << 20, 2 * pl), batch_pieces=64) as pool:
+        for rep in range(2):
+            sp, taken, bad = _run_split(pool, paths, sizes, pl, exp, first, end, cpu_threads,
+                                        rate=rng.choice([0.0, 5e8, 4e9]))
+            b = sp.boundary
+            assert first <= b <= end and taken == b - first
+            if cpu_threads == 0:
+                assert b == first  # no pool: the engine took every piece
+            assert sp.verdicts() == want[first:end], (seed, rep, b)
+            st = pool.stats()
+            assert st["io_errors"] >= bad
+
+
+def test_split_whole_range_both_sides_take_part(built, gpu, tmp_path):
+    """A torrent large enough that both sides finish work: 384 x 2 MiB, one
+    damaged piece near each end; the pool at 8 threads (its rate measured in
+    the call) and the engine both take pieces."""
+    from vortex_amd.hash_pool import HashPool
+
+    pl, n = 2 << 20, 384
+    paths, sizes, exp = _files(tmp_path, pl, [n * pl - 12345], 99)
+    for off in (3 * pl + 17, (n - 3) * pl + 5):
+        with open(paths[0], "r+b") as f:
+            f.seek(off)
+            b = f.read(1)
+            f.seek(off)
+            f.write(bytes([b[0] ^ 1]))
+    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=8)
+    with HashPool(pl, slots=4, slot_bytes=256 << 20, batch_pieces=1024) as pool:
+        pool.verify_files(paths, sizes, pl, exp, io_threads=8)  # warm the stages and the page cache
+        for _ in range(3):
+            sp, taken, bad = _run_split(pool, paths, sizes, pl, exp, 0, n, 8, io_threads=8)
+            assert sp.verdicts() == want and bad == 0
+            assert 0 < sp.boundary < n, sp.boundary  # both sides took part
+            rounds = pool.last_verify_rounds()
+            assert rounds and sum(r["bytes"] for r in rounds) >= (n - sp.boundary) * pl - 12345
+
+
+def test_split_engine_failure_leaves_its_pieces_to_the_caller(built, gpu, tmp_path):
+    """An engine round that fails (injected) returns the error; the pool
+    still finishes its side, and the pieces [boundary, end) — the ones with
+    no verdict — are what the caller verifies itself (vx_hash.h)."""
+    from vortex_amd._lib import VX_EDEVICE, VxError
+    from vortex_amd.hash_pool import HashPool
+
+    pl, n = 1 << 20, 96
+    paths, sizes, exp = _files(tmp_path, pl, [n * pl], 5)
+    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
+    with HashPool(pl, slots=3, slot_bytes=32 << 20, batch_pieces=64, verify_chunk=131072, hooks=True) as pool:
+        pool.lib.vx_tuning_fail_launch_after(pool._h, 3)
+        with pytest.raises(VxError) as ei:
+            _run_split(pool, paths, sizes, pl, exp, 0, n, 2)
+        assert ei.value.code == VX_EDEVICE
+        # the same context, next call: a clean split
+        sp, taken, bad = _run_split(pool, paths, sizes, pl, exp, 0, n, 2)
+        assert sp.verdicts() == want and bad == 0

@@ -45,6 +45,7 @@ EXPORTS = (
     "vx_sha1_device_uniform", "vx_sha1_device_ragged", "vx_sha1_device_ragged_hint", "vx_sort_order",
     "vx_plan_verify", "vx_plan_verify_gpus", "vx_plan_verify_split", "vx_get_stats", "vx_reset_stats",
     "vx_last_verify", "vx_last_verify_rounds",
+    "vx_split_init", "vx_split_claim", "vx_split_done", "vx_split_boundary", "vx_verify_files_split",
 )
 # ... plus include/vx_tuning.h and include/vx_synth.h: libvortex_amd_tuning.so only.
 TUNING_EXPORTS = (
@@ -52,7 +53,8 @@ TUNING_EXPORTS = (
     "vx_tuning_zero_copy_plan", "vx_tuning_zero_copy_kernel", "vx_tuning_plan_ragged", "vx_tuning_chunk_schedule",
     "vx_tuning_fail_submit_after", "vx_tuning_fail_launch_after", "vx_tuning_verify_copy_stream", "vx_tuning_stage_huge",
     "vx_tuning_clock_stamp",
-    "vx_tuning_wall_clock_khz", "vx_tuning_device_identity",
+    "vx_tuning_wall_clock_khz", "vx_tuning_device_identity", "vx_tuning_split_take_tail",
+    "vx_tuning_last_split",
 )
 
 
@@ -117,6 +119,13 @@ class vx_verify_round(ctypes.Structure):
         ("flags", ctypes.c_uint32)]
 
 
+class vx_split(ctypes.Structure):
+    """The split's claim word and the pool's progress (include/vx_hash.h)."""
+    _fields_ = [("word", ctypes.c_uint64), ("pool_done", ctypes.c_uint64), ("start_ns", ctypes.c_uint64),
+                ("first", ctypes.c_uint64), ("end", ctypes.c_uint64), ("cpu_threads", ctypes.c_uint32),
+                ("_pad", ctypes.c_uint32), ("cpu_thread_rate", ctypes.c_double)]
+
+
 _lib = None
 _tuning = None
 _lock = threading.Lock()
@@ -163,6 +172,12 @@ def _declare(L: ctypes.CDLL, tuning: bool = False) -> None:
                                  c.POINTER(vx_plan)], c.c_int),
         "vx_plan_verify_split": ([c.c_uint64, c.c_uint32, c.c_uint64, c.c_uint32, c.c_double, c.c_uint32,
                                   c.POINTER(c.c_uint64), c.POINTER(c.c_uint64), c.POINTER(vx_plan)], c.c_int),
+        "vx_split_init": ([c.POINTER(vx_split), c.c_uint64, c.c_uint64, c.c_uint32, c.c_double], c.c_int),
+        "vx_split_claim": ([c.POINTER(vx_split)], c.c_int64),
+        "vx_split_done": ([c.POINTER(vx_split), c.c_uint64], None),
+        "vx_split_boundary": ([c.POINTER(vx_split)], c.c_uint64),
+        "vx_verify_files_split": ([vp, vp, vp, c.c_size_t, c.c_uint32, vp, c.c_size_t, c.POINTER(vx_split), vp,
+                                   c.c_uint32], c.c_int64),
     }
     if tuning:
         sig.update({
@@ -179,6 +194,8 @@ def _declare(L: ctypes.CDLL, tuning: bool = False) -> None:
             "vx_tuning_wall_clock_khz": ([c.c_int], c.c_int),
             "vx_tuning_device_identity": ([c.c_int, c.c_char_p, c.c_size_t, c.c_char_p], c.c_int),
             "vx_tuning_plan_ragged": ([c.c_uint32, c.c_uint32, c.c_uint64], c.c_int),
+            "vx_tuning_split_take_tail": ([c.POINTER(vx_split), c.c_uint64], c.c_uint64),
+            "vx_tuning_last_split": ([vp, c.POINTER(c.c_double), c.c_size_t], c.c_size_t),
             "vx_tuning_chunk_schedule": ([c.c_uint64, c.c_uint64, c.c_int, c.c_int, c.POINTER(c.c_uint64),
                                           c.c_size_t], c.c_size_t),
             "vx_synth_fill": ([vp, c.c_uint64, c.c_uint32, c.c_uint32, c.c_uint64, c.c_uint64, c.c_uint32, vp],

@@ -210,6 +210,13 @@ struct vx_ctx {
     vx_verify_trace last_verify{};
     std::vector<hipEvent_t> copy_ev;
     std::vector<vx_verify_round> last_rounds;  // vx_last_verify_rounds
+    // the last split call's decisions, one per round formed (vx_tuning_last_split)
+    struct SplitDecision {
+        double t_ms, pool_rate, engine_rate, block_ns, t_engine_ms, t_pool_ms;
+        uint64_t unclaimed, group, lanes, pool_done;
+        uint32_t mode, measured;
+    };
+    std::vector<SplitDecision> last_split;
     // The file re-verify's chunk rounds put every H2D on this one stream (high
     // priority: its own hardware queue) and only kernels on the slot streams,
     // so no copy ever sits behind a kernel.  Created on first
@@ -1430,21 +1437,27 @@ struct ChunkPipe {
     // Wait for every round, then copy verdicts / digests back (either may be
     // NULL).  bad (may be NULL): pieces the caller fails for an I/O error,
     // counted in io_errors and not again as mismatches.
-    int finish(uint8_t* matched_out, uint8_t* digests_out, int rc, const uint8_t* bad = nullptr) {
+    // Only rows [lo, hi) are the call's (the split: the engine's pieces).
+    int finish(uint8_t* matched_out, uint8_t* digests_out, int rc, const uint8_t* bad = nullptr, uint64_t lo = 0,
+               uint64_t hi = UINT64_MAX) {
+        hi = std::min(hi, cnt);
+        lo = std::min(lo, hi);
         if (!rc) {
             for (auto& s : c->slots)
                 if (s.state == Slot::INFLIGHT && hipEventSynchronize(s.done) != hipSuccess) rc = VX_EDEVICE;
             if (rc) (void)fail(rc, "chunk rounds failed on device");
         }
-        if (!rc && matched_out && d_match && hipMemcpy(matched_out, d_match, cnt, hipMemcpyDeviceToHost) != hipSuccess)
+        if (!rc && matched_out && d_match && hi > lo &&
+            hipMemcpy(matched_out + lo, d_match + lo, hi - lo, hipMemcpyDeviceToHost) != hipSuccess)
             rc = fail(VX_EDEVICE, "verdict D2H failed");
-        if (!rc && digests_out && hipMemcpy(digests_out, d_dig, cnt * 20, hipMemcpyDeviceToHost) != hipSuccess)
+        if (!rc && digests_out && hi > lo &&
+            hipMemcpy(digests_out + 20 * lo, d_dig + 20 * lo, (hi - lo) * 20, hipMemcpyDeviceToHost) != hipSuccess)
             rc = fail(VX_EDEVICE, "digest D2H failed");
         if (!rc) {
-            c->stats.pieces_completed += cnt;
+            c->stats.pieces_completed += hi - lo;
             c->stats.bytes_completed += bytes;
             if (matched_out && d_match)
-                for (uint64_t i = 0; i < cnt; ++i) c->stats.pieces_mismatched += matched_out[i] == 0 && !(bad && bad[i]);
+                for (uint64_t i = lo; i < hi; ++i) c->stats.pieces_mismatched += matched_out[i] == 0 && !(bad && bad[i]);
         }
         for (auto& s : c->slots)
             if (s.state == Slot::INFLIGHT) {
@@ -1681,6 +1694,417 @@ int verify_chunked(FileVerify& fv, vx_files::Readers& rd, uint64_t n, uint32_t p
         for (uint64_t i = 0; i < cnt; ++i)
             if (fv.bad[i]) fv.matched_out[i] = 0;
     fv.done = cnt;
+    return rc;
+}
+
+// The GPU's per-block chain time on the split kernels and the PCIe rate: the
+// cost model's hardware figures (vx_plan_verify), and the
+// split's cold-start guesses before it has measured its own.
+constexpr double kChainBlock = 0.76e-6, kPcieRate = 52.0 * (1ull << 30);
+
+// ---- the self-balancing split (vx_verify_files_split) ----
+// The claim word: head (low 32 bits) | stop (high 32).  The pool moves head
+// up one piece per compare-and-swap (vx_split_claim); the engine moves stop
+// down by a group (split_take_tail).  Neither side can take a piece the other
+// has, and a group the engine asks for is cut to what is still unclaimed.
+uint64_t split_take_tail(vx_split* s, uint64_t k) {
+    uint64_t w = __atomic_load_n(&s->word, __ATOMIC_ACQUIRE);
+    for (;;) {
+        const uint64_t head = w & 0xffffffffull, stop = w >> 32;
+        const uint64_t take = std::min(k, stop > head ? stop - head : 0);
+        if (take == 0) return stop;
+        const uint64_t nw = head | ((stop - take) << 32);
+        if (__atomic_compare_exchange_n(&s->word, &w, nw, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE))
+            return stop - take;
+    }
+}
+
+// Streaming chunk rounds over pieces the engine claims from the top of the
+// split as it goes.  A claimed piece takes a lane from its first chunk to its
+// last, one C-byte chunk per round; every round carries all active lanes and
+// the group that joins it (batch_chunked_gather's streaming rounds, here with
+// the group sized at run time).  Before forming a round the engine estimates
+//   T_engine(j) = the rounds its lanes (and j new pieces) still need, each
+//                 max(bytes / min(copy rate, read rate), longest chunk's chain)
+//   T_pool(j)   = (unclaimed - j + the pool's pieces in hand) / pool rate
+// and takes the largest j with T_engine(j) <= T_pool(j).  Every rate is
+// measured in this call: the copy rate and the chain per 64-byte block from
+// the GPU events around each round's copy and kernel, the read rate from the
+// readers' busy time, the pool's rate from vx_split_done.  The first group
+// comes from the cold-start rates (the caller's per-thread rate, the PCIe
+// rate, the kernel's chain per block); no other group is formed until both
+// sides have measured rates.  The engine's pieces are the contiguous tail
+// [*lowest, end) of the range.
+int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n, uint32_t pl, uint64_t total,
+                 uint64_t C, uint64_t* lowest) {
+    vx_ctx* c = fv.c;
+    const uint64_t first = sp->first, end = sp->end, cnt = end - first;
+    const uint64_t last_len = total - (n - 1) * (uint64_t)pl;
+    auto plen = [&](uint64_t i) { return i == n - 1 ? last_len : (uint64_t)pl; };
+    ChunkPipe cp(c);
+    c->last_split.clear();
+    int rc = cp.open(cnt, fv.expected + 20 * first, "vx_verify_files_split");
+    if (!rc && c->verify_copy_stream) rc = cp.use_copy_stream();
+    const uint64_t longest = std::max<uint64_t>(pl, last_len);
+    const uint64_t pitch = align_up(std::min<uint64_t>(C, longest), vx_files::DirectIo::kBlock);
+    const Slot& s0 = c->slots[0];
+    const uint64_t max_lanes = std::max<uint64_t>(1, std::min<uint64_t>(s0.cap, s0.arena_cap / pitch));
+    *lowest = end;
+
+    struct Lane {
+        uint64_t piece, a;
+        bool ramp;  // joined in the first round: chunks C/4, C/4, C/2, then C
+    };
+    std::vector<Lane> act;  // claimed pieces with chunks left, in join order
+    // The first group's head ramp (verify_chunked's, per lane): its first
+    // round is a C/4 chain and a quarter of the bytes, so the call's first
+    // read and the copy that nothing overlaps are short.  Later groups join
+    // rounds whose chain is C anyway, and a ramp would only add rounds.
+    const bool ramp_ok = C >= 4 * vx_files::DirectIo::kBlock;
+    auto chunk_len = [&](uint64_t L, uint64_t a, bool ramp) {
+        uint64_t k = C;
+        if (ramp && ramp_ok && L >= 2 * C) k = a < C / 2 ? C / 4 : a < C ? C / 2 : C;
+        return std::min<uint64_t>(k, L - a);
+    };
+    // chunk lengths of a full-length piece joining now (ramped or not)
+    auto schedule = [&](bool ramp) {
+        std::vector<uint64_t> v;
+        for (uint64_t a = 0; a < pl;) v.push_back(chunk_len(pl, a, ramp)), a += v.back();
+        if (v.empty()) v.push_back(0);
+        return v;
+    };
+    const std::vector<uint64_t> sched_plain = schedule(false), sched_ramp = schedule(true);
+    struct Round {
+        int si = -1;
+        uint32_t m = 0;
+        bool continues = false;
+        uint64_t ticket = 0, bytes = 0, max_chunk = 0, t_submit = 0;
+    };
+    std::deque<Round> formed;  // reads queued, not yet enqueued
+    const size_t nslots = c->slots.size();
+    const size_t depth = nslots > 1 ? std::min<size_t>(kReadahead, nslots - 1) : 0;
+    std::vector<std::vector<vx_files::ReadItem>> items(nslots);
+    using clk = std::chrono::steady_clock;
+    // enqueued rounds: bytes, longest chunk, timing-event index (-1: untimed)
+    struct Sent {
+        uint64_t bytes, max_chunk;
+        long ev;
+        bool continues;
+    };
+    std::vector<Sent> sent;
+    size_t timed = 0, measured_upto = 0;  // rounds [0, measured_upto) are in the rates below
+    double copy_bytes = 0, copy_ms = 0;   // measured copies
+    std::vector<double> block_ns;         // measured chain per 64-byte block, one per round
+    std::vector<uint64_t> timed_bytes;
+    std::vector<vx_verify_round> tl;
+    std::vector<long> tl_ev;
+    bool anchored = false;
+    uint64_t t_anchor = 0;
+    if (c->anchor_ev || hipEventCreate(&c->anchor_ev) == hipSuccess) {
+        anchored = hipEventRecord(c->anchor_ev, c->slots[0].stream) == hipSuccess;
+        t_anchor = vx_files::Readers::now_ns();
+    }
+    auto rel_ms = [&](uint64_t t_ns) { return t_ns ? ((double)t_ns - (double)c->verify_t0_ns) * 1e-6 : 0.0; };
+    auto consume = [&] { fv.consume(); };
+    const double pool_threads = sp->cpu_threads;
+    const double pool_rate0 = pool_threads * (sp->cpu_thread_rate > 0 ? sp->cpu_thread_rate : 2.2e9) / (double)pl;
+
+    // Fold newly finished rounds into the copy and chain rates (events are
+    // queried, never waited for).
+    size_t copied_upto = 0;  // rounds whose copy is in copy_bytes / copy_ms
+    auto measure = [&] {
+        // copies as soon as they end (the first rate arrives a kernel earlier)
+        while (copied_upto < sent.size()) {
+            const Sent& r = sent[copied_upto];
+            if (r.ev >= 0) {
+                const size_t e = 3 * (size_t)r.ev;
+                if (hipEventQuery(c->copy_ev[e + 1]) != hipSuccess) break;
+                float cm = 0;
+                if (hipEventElapsedTime(&cm, c->copy_ev[e], c->copy_ev[e + 1]) == hipSuccess && cm > 0) {
+                    copy_bytes += (double)r.bytes;
+                    copy_ms += cm;
+                }
+            }
+            ++copied_upto;
+        }
+        // kernels: the chain per block, and which rounds are done
+        while (measured_upto < sent.size()) {
+            const Sent& r = sent[measured_upto];
+            if (r.ev < 0) {
+                ++measured_upto;
+                continue;
+            }
+            const size_t e = 3 * (size_t)r.ev;
+            if (hipEventQuery(c->copy_ev[e + 2]) != hipSuccess) break;  // kernel not done yet
+            float k0 = 0, k1 = 0, ce = 0;
+            // the kernel starts after its copy and, when its lanes continue, after
+            // the previous round's kernel
+            long prev = -1;
+            for (size_t k = measured_upto; r.continues && k-- > 0;)
+                if (sent[k].ev >= 0) {
+                    prev = sent[k].ev;
+                    break;
+                }
+            if (hipEventElapsedTime(&ce, c->copy_ev[0], c->copy_ev[e + 1]) == hipSuccess &&
+                hipEventElapsedTime(&k1, c->copy_ev[0], c->copy_ev[e + 2]) == hipSuccess) {
+                if (prev >= 0) (void)hipEventElapsedTime(&k0, c->copy_ev[0], c->copy_ev[3 * (size_t)prev + 2]);
+                const double kern_ms = (double)k1 - std::max<double>(ce, prev >= 0 ? k0 : 0.0);
+                const double blocks = (double)((r.max_chunk + 63) / 64);
+                if (kern_ms > 0 && blocks > 0) block_ns.push_back(kern_ms * 1e6 / blocks);
+            }
+            ++measured_upto;
+        }
+    };
+    // How many pieces to take now (0..room).
+    // mode 0: a round after the first (no group until both sides have rates);
+    // 1: the first round (the cold-start answer); 2: nothing is in flight and
+    // the rates are not all in: decide with what there is.
+    auto decide = [&](uint64_t room, int mode, bool* measured) -> uint64_t {
+        measure();
+        const uint64_t w = __atomic_load_n(&sp->word, __ATOMIC_ACQUIRE);
+        const uint64_t head = w & 0xffffffffull, stop = w >> 32;
+        const uint64_t unclaimed = stop > head ? stop - head : 0;
+        if (unclaimed == 0 || room == 0) return 0;
+        const uint64_t done = __atomic_load_n(&sp->pool_done, __ATOMIC_ACQUIRE);
+        const double el = ((double)vx_files::Readers::now_ns() - (double)sp->start_ns) * 1e-9;
+        const bool pool_measured = pool_threads == 0 || (done >= std::max(4.0, pool_threads) && el > 0);
+        const double p = pool_threads == 0 ? 0.0 : pool_measured ? (double)done / el : pool_rate0;
+        const double in_hand = (double)(head - first) - (double)std::min<uint64_t>(done, head - first);
+        // The engine counts as measured once one copy is timed: its chain per
+        // block is a property of the kernel, known within a few % before any
+        // round of this call ends (kChainBlock), and waiting for a kernel end
+        // put the first measured group a whole round later.
+        *measured = copy_ms > 0 && pool_measured;
+        if (!*measured && mode == 0) return 0;
+        // engine rates
+        double rin = copy_ms > 0 ? copy_bytes / (copy_ms * 1e-3) : kPcieRate;
+        if (rd.busy_ns() > 0 && rd.threads() > 0)
+            rin = std::min(rin, (double)rd.bytes_read() / ((double)rd.busy_ns() * 1e-9 / (double)rd.threads()));
+        double bns = kChainBlock * 1e9;
+        if (!block_ns.empty()) {
+            std::vector<double> b = block_ns;
+            std::nth_element(b.begin(), b.begin() + b.size() / 2, b.end());
+            bns = b[b.size() / 2];
+        }
+        auto round_s = [&](double bytes, uint64_t chunk) {
+            return std::max(bytes / rin, (double)((chunk + 63) / 64) * bns * 1e-9);
+        };
+        // rounds queued ahead of the new group (formed, or enqueued and not measured)
+        double t_queued = 0;
+        for (const Round& r : formed) t_queued += round_s((double)r.bytes, r.max_chunk);
+        for (size_t k = measured_upto; k < sent.size(); ++k) t_queued += round_s((double)sent[k].bytes, sent[k].max_chunk);
+        // future rounds of the active lanes: bytes per round index
+        std::vector<double> fut;
+        std::vector<uint64_t> fut_max;  // each future round's longest chunk
+        for (const Lane& l : act) {
+            const uint64_t L = plen(l.piece);
+            uint64_t a = l.a;
+            for (size_t r = 0; a < L; ++r) {
+                const uint64_t k = chunk_len(L, a, l.ramp);
+                if (fut.size() <= r) fut.resize(r + 1, 0.0), fut_max.resize(r + 1, 0);
+                fut[r] += (double)k;
+                fut_max[r] = std::max(fut_max[r], k);
+                a += k;
+            }
+        }
+        const std::vector<uint64_t>& js = mode == 1 ? sched_ramp : sched_plain;
+        auto t_engine = [&](uint64_t j) {
+            double t = t_queued;
+            const size_t R = std::max<size_t>(fut.size(), j ? js.size() : 0);
+            for (size_t r = 0; r < R; ++r) {
+                double b = r < fut.size() ? fut[r] : 0.0;
+                uint64_t k = r < fut_max.size() ? fut_max[r] : 0;
+                if (j && r < js.size()) b += (double)j * (double)js[r], k = std::max(k, js[r]);
+                if (b > 0) t += round_s(b, k);
+            }
+            return t;
+        };
+        auto t_pool = [&](uint64_t j) {
+            return p > 0 ? ((double)(unclaimed - j) + in_hand) / p : std::numeric_limits<double>::infinity();
+        };
+        // the largest j in [0, min(unclaimed, room)] with t_engine(j) <= t_pool(j):
+        // t_engine grows with j and t_pool shrinks, so bisect
+        auto ok = [&](uint64_t j) { return t_engine(j) <= t_pool(j); };
+        uint64_t lo = 0, hi = std::min(unclaimed, room);
+        if (ok(hi)) {
+            lo = hi;
+        } else if (ok(1)) {
+            lo = 1;
+            while (lo + 1 < hi) {
+                const uint64_t mid = lo + (hi - lo) / 2;
+                (ok(mid) ? lo : hi) = mid;
+            }
+        }
+
+        c->last_split.push_back(vx_ctx::SplitDecision{
+            ((double)vx_files::Readers::now_ns() - (double)c->verify_t0_ns) * 1e-6, p, rin, bns,
+            t_engine(lo) * 1e3, t_pool(lo) * 1e3, unclaimed, lo, (uint64_t)act.size(), done, (uint32_t)mode,
+            *measured ? 1u : 0u});
+        return lo;
+    };
+
+    // Form the next round into a slot: the active lanes' next chunks plus a
+    // group claimed now.  1 = formed, 0 = nothing left for the engine,
+    // -1 = no slot free (block = false) or an error (rc set).
+    bool formed_any = false;
+    auto form = [&](bool block) -> int {
+        int si = -1;
+        for (int attempt = 0;; ++attempt) {
+            if (block) {
+                si = cp.free_slot(consume);
+                if (si < 0) {
+                    rc = si;
+                    return -1;
+                }
+            } else {
+                if ((rc = cp.try_free_slot(&si, consume))) return -1;
+                if (si < 0) return -1;
+            }
+            bool measured = false;
+            bool inflight = false;
+            for (const Slot& q : c->slots) inflight |= q.state == Slot::INFLIGHT;
+            const int mode = !formed_any && attempt == 0 ? 1 : (block && !inflight && formed.empty()) ? 2 : 0;
+            const uint64_t j = decide(max_lanes - std::min<uint64_t>(max_lanes, act.size()), mode, &measured);
+            if (j > 0 || !act.empty()) {
+                Slot& s = c->slots[si];
+                reset_fill(s);
+                if ((rc = ensure_stage(c, s))) return -1;
+                auto& it = items[si];
+                it.clear();
+                // the round's lanes: the active ones, then the group claimed now
+                std::vector<Lane> lanes = act;
+                const bool continues = !act.empty();
+                if (j) {
+                    const uint64_t old = *lowest;  // the engine alone lowers stop: it is still here
+                    const uint64_t lo = split_take_tail(sp, j);
+                    for (uint64_t i = lo; i < old; ++i) lanes.push_back(Lane{i, 0, !formed_any});
+                    *lowest = std::min(*lowest, lo);
+                }
+                // lanes sit one round pitch apart: the round's longest chunk,
+                // 4 KiB aligned for O_DIRECT (ramp rounds copy no gaps)
+                uint64_t max_chunk = 0;
+                for (const Lane& l : lanes) max_chunk = std::max(max_chunk, chunk_len(plen(l.piece), l.a, l.ramp));
+                const uint64_t rp = std::max<uint64_t>(vx_files::DirectIo::kBlock,
+                                                       align_up(max_chunk, vx_files::DirectIo::kBlock));
+                uint32_t m = 0;
+                std::vector<Lane> keep;
+                for (const Lane& l : lanes) {
+                    const uint64_t L = plen(l.piece), clen = chunk_len(L, l.a, l.ramp);
+                    it.push_back(vx_files::ReadItem{s.h_stage + (uint64_t)m * rp, l.piece, l.a, clen});
+                    s.h_offsets[m] = (uint64_t)m * rp;
+                    s.h_lens[m] = (uint32_t)clen;
+                    s.h_pidx[m] = (uint32_t)(l.piece - first);
+                    s.h_poff[m] = l.a;
+                    s.h_tlen[m] = L;
+                    ++m;
+                    if (l.a + clen < L) keep.push_back(Lane{l.piece, l.a + clen, l.ramp});
+                }
+                act.swap(keep);
+                if (m == 0) continue;  // the group came back empty (the pool took the rest)
+                formed_any = true;
+                s.state = Slot::FILLING;  // reserved until the round is enqueued
+                Round r;
+                r.si = si;
+                r.m = m;
+                r.continues = continues;
+                r.bytes = s.bytes = (uint64_t)(m - 1) * rp + s.h_lens[m - 1];
+                r.max_chunk = max_chunk;
+                r.t_submit = vx_files::Readers::now_ns();
+                r.ticket = rd.submit(it);
+                formed.push_back(r);
+                return 1;
+            }
+            // Nothing to form.  While the rates are not all in, wait for a round
+            // in flight and decide again (mode 2 once none is left); with
+            // them, the engine is done: the pool takes the rest.
+            if (!block || measured || mode == 2) return 0;
+            if (inflight) {
+                if ((rc = reap(c, true))) return -1;
+                consume();
+            }
+        }
+    };
+
+    auto t_last_enqueue = clk::now();
+    for (;;) {
+        while (formed.size() <= depth) {
+            const int f = form(formed.empty());
+            if (f <= 0) break;
+        }
+        if (rc || formed.empty()) break;
+        Round r = formed.front();
+        formed.pop_front();
+        rd.wait(r.ticket);
+        vx_verify_round vr{};
+        vr.read_submit_ms = rel_ms(r.t_submit);
+        vr.read_done_ms = rel_ms(rd.done_ns(r.ticket));
+        vr.enqueue_ms = rel_ms(vx_files::Readers::now_ns());
+        vr.bytes = r.bytes;
+        vr.lanes = r.m;
+        vr.flags = r.continues ? 0u : VX_ROUND_NEW_WINDOW;
+        long ev_k = -1;
+        rc = cp.round(r.si, r.m, r.continues, false, [&](Slot& sl, hipStream_t st) {
+            bool ev = true;
+            while (ev && c->copy_ev.size() < 3 * timed + 3) {
+                hipEvent_t e = nullptr;
+                ev = hipEventCreate(&e) == hipSuccess;
+                if (ev) c->copy_ev.push_back(e);
+            }
+            ev = ev && hipEventRecord(c->copy_ev[3 * timed], st) == hipSuccess;
+            if (hipMemcpyAsync(sl.d_arena, sl.h_stage, sl.bytes, hipMemcpyHostToDevice, st) != hipSuccess)
+                return fail(VX_EDEVICE, "vx_verify_files_split: chunk H2D failed");
+            if (ev && hipEventRecord(c->copy_ev[3 * timed + 1], st) == hipSuccess) {
+                timed_bytes.push_back(sl.bytes);
+                cp.copy_end = c->copy_ev[3 * timed + 1];
+                ev_k = (long)timed++;
+            }
+            return 0;
+        });
+        if (!rc && ev_k >= 0 && hipEventRecord(c->copy_ev[3 * ev_k + 2], c->slots[r.si].stream) != hipSuccess)
+            ev_k = -1;
+        sent.push_back(Sent{r.bytes, r.max_chunk, ev_k, r.continues});
+        tl.push_back(vr);
+        tl_ev.push_back(ev_k);
+        t_last_enqueue = clk::now();
+        if (rc) break;
+    }
+    rd.wait();  // error path: no read may still target a stage
+    for (auto& sl : c->slots)
+        if (sl.state == Slot::FILLING) {
+            reset_fill(sl);
+            sl.state = Slot::FREE;
+        }
+    const uint64_t lo_row = *lowest - first;
+    for (uint64_t i = *lowest; i < end; ++i) cp.bytes += plen(i);
+    rc = cp.finish(fv.matched_out, nullptr, rc, fv.bad.data(), lo_row, cnt);
+    vx_verify_trace& vt = c->last_verify;
+    vt.tail_ms = std::chrono::duration<double, std::milli>(clk::now() - t_last_enqueue).count();
+    if (!rc && timed) {
+        float a = 0, b = 0, busy = 0;
+        for (size_t k = 0; k < timed; ++k) {
+            (void)hipEventElapsedTime(&a, c->copy_ev[0], c->copy_ev[3 * k]);
+            (void)hipEventElapsedTime(&b, c->copy_ev[0], c->copy_ev[3 * k + 1]);
+            busy += b - a;
+            vt.copy_bytes += timed_bytes[k];
+        }
+        vt.copy_busy_ms = busy;
+        vt.copy_span_ms = b;
+        vt.rounds = (uint32_t)timed;
+        const double base = anchored ? ((double)t_anchor - (double)c->verify_t0_ns) * 1e-6 : 0.0;
+        for (size_t k = 0; k < tl.size() && anchored; ++k) {
+            if (tl_ev[k] < 0) continue;
+            float x = 0;
+            const size_t e = 3 * (size_t)tl_ev[k];
+            if (hipEventElapsedTime(&x, c->anchor_ev, c->copy_ev[e]) == hipSuccess) tl[k].copy_start_ms = base + x;
+            if (hipEventElapsedTime(&x, c->anchor_ev, c->copy_ev[e + 1]) == hipSuccess) tl[k].copy_end_ms = base + x;
+            if (hipEventElapsedTime(&x, c->anchor_ev, c->copy_ev[e + 2]) == hipSuccess) tl[k].kernel_end_ms = base + x;
+        }
+    }
+    c->last_rounds = std::move(tl);
+    if (!rc)
+        for (uint64_t i = lo_row; i < cnt; ++i)
+            if (fv.bad[i]) fv.matched_out[i] = 0;
+    fv.done = cnt - lo_row;
     return rc;
 }
 
@@ -1963,9 +2387,11 @@ int vx_verify_batch(vx_ctx* c, const uint8_t* const* ptrs, const uint32_t* lens,
 }
 
 
-int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
-                              uint32_t piece_length, const uint8_t* expected, size_t n_pieces, size_t first,
-                              size_t count, uint8_t* matched_out, uint32_t io_threads) {
+// vx_verify_files_range, and with sp the engine's side of a split
+// (vx_verify_files_split: pieces [sp->first, sp->end), always chunk rounds).
+static int64_t verify_files_impl(vx_ctx* c, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
+                                 uint32_t piece_length, const uint8_t* expected, size_t n_pieces, size_t first,
+                                 size_t count, uint8_t* matched_out, uint32_t io_threads, vx_split* sp) {
     if (!c || (nfiles && (!paths || !file_lengths)) || piece_length == 0 || (n_pieces && !expected) ||
         (count && !matched_out))
         return fail(VX_EINVAL, "vx_verify_files: bad argument");
@@ -1979,9 +2405,10 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
         return fail(VX_EINVAL, "vx_verify_files: n_pieces does not match the files' total length");
     if (count == 0) return 0;
     const uint64_t C = verify_chunk_for(c, count);
-    bool chunked = piece_length >= 2 * C;
+    bool chunked = piece_length >= 2 * C || sp;  // the split always streams chunk rounds
     if (piece_length > c->cfg.max_piece_len) chunked = true;  // whole pieces would not fit a slot
-    if (chunked ? c->slots[0].arena_cap < C : piece_length > c->cfg.max_piece_len)
+    if (chunked ? c->slots[0].arena_cap < std::min<uint64_t>(C, align_up(piece_length, vx_files::DirectIo::kBlock))
+                : piece_length > c->cfg.max_piece_len)
         return fail(VX_ERANGE, "vx_verify_files: pieces do not fit the context's slots");
     int rc = set_device(c);
     if (rc) return rc;
@@ -1996,7 +2423,7 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
     for (size_t f = 0; f < nfiles; ++f) fds[f] = open(paths[f], O_RDONLY | O_CLOEXEC);
     const int nthreads = io_threads ? (int)io_threads : (int)std::max(1u, std::min(16u, usable_cpus()));
     std::vector<uint8_t> bad(count, 0);
-    std::memset(matched_out, 0, count);
+    if (!sp) std::memset(matched_out, 0, count);  // (the split's pool writes its entries concurrently)
     {
         const vx_files::DirectIo dio(fds, c->cfg.direct_io != 0);
         vx_files::Readers rd(nthreads, fs, fds, piece_length, bad.data(), first, &dio);
@@ -2010,8 +2437,11 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
                                 ? Cc
                                 : C;
         c->last_verify.chunk_bytes = chunked ? Cv : 0;
-        rc = chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total, first, end, Cv)
-                     : verify_whole(fv, rd, n_pieces, piece_length, total, first, end);
+        uint64_t lowest = end;
+        rc = sp        ? verify_split(fv, rd, sp, n_pieces, piece_length, total, Cv, &lowest)
+             : chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total, first, end, Cv)
+                       : verify_whole(fv, rd, n_pieces, piece_length, total, first, end);
+        if (sp) std::fill(bad.begin(), bad.begin() + (lowest - first), 0);  // the pool's pieces: its own errors
         if (!rc && !chunked) {
             while (fv.done < count && !rc) {
                 rc = reap(c, true);
@@ -2053,6 +2483,53 @@ int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_
     for (uint8_t x : bad) nbad += x;
     c->stats.io_errors += (uint64_t)nbad;
     return nbad;
+}
+
+int64_t vx_verify_files_range(vx_ctx* c, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
+                              uint32_t piece_length, const uint8_t* expected, size_t n_pieces, size_t first,
+                              size_t count, uint8_t* matched_out, uint32_t io_threads) {
+    return verify_files_impl(c, paths, file_lengths, nfiles, piece_length, expected, n_pieces, first, count,
+                             matched_out, io_threads, nullptr);
+}
+
+int vx_split_init(vx_split* s, uint64_t first, uint64_t end, uint32_t cpu_threads, double cpu_thread_rate) {
+    if (!s || first > end || end > 0xffffffffull) return fail(VX_EINVAL, "vx_split_init: bad range");
+    if (!(cpu_thread_rate >= 0)) return fail(VX_EINVAL, "vx_split_init: cpu_thread_rate must be >= 0");
+    *s = vx_split{};
+    s->first = first;
+    s->end = end;
+    s->cpu_threads = cpu_threads;
+    s->cpu_thread_rate = cpu_thread_rate;
+    s->start_ns = vx_files::Readers::now_ns();
+    __atomic_store_n(&s->word, first | (end << 32), __ATOMIC_RELEASE);
+    return 0;
+}
+
+int64_t vx_split_claim(vx_split* s) {
+    if (!s) return -1;
+    uint64_t w = __atomic_load_n(&s->word, __ATOMIC_ACQUIRE);
+    for (;;) {
+        const uint64_t head = w & 0xffffffffull, stop = w >> 32;
+        if (head >= stop) return -1;
+        if (__atomic_compare_exchange_n(&s->word, &w, w + 1, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE))
+            return (int64_t)head;
+    }
+}
+
+void vx_split_done(vx_split* s, uint64_t pieces) {
+    if (s) __atomic_fetch_add(&s->pool_done, pieces, __ATOMIC_RELEASE);
+}
+
+uint64_t vx_split_boundary(const vx_split* s) {
+    return s ? __atomic_load_n(&s->word, __ATOMIC_ACQUIRE) >> 32 : 0;
+}
+
+int64_t vx_verify_files_split(vx_ctx* c, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
+                              uint32_t piece_length, const uint8_t* expected, size_t n_pieces, vx_split* s,
+                              uint8_t* matched_out, uint32_t io_threads) {
+    if (!s || s->first > s->end || s->end > n_pieces) return fail(VX_EINVAL, "vx_verify_files_split: bad split");
+    return verify_files_impl(c, paths, file_lengths, nfiles, piece_length, expected, n_pieces, s->first,
+                             s->end - s->first, matched_out, io_threads, s);
 }
 
 int64_t vx_verify_files(vx_ctx* c, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
@@ -2194,7 +2671,7 @@ int vx_plan_verify(uint64_t n_pieces, uint32_t piece_length, uint64_t total_leng
 // host with many cores can keep its pool against any number of GPUs when the
 // pieces are long (INTEGRATION.md "A whole node is a different host").
 namespace {
-constexpr double kChainBlock = 0.76e-6, kPcieRate = 52.0 * (1ull << 30), kSetup = 1.5e-3;
+constexpr double kSetup = 1.5e-3;
 constexpr double kOverlapLoss = 0.08, kMargin = 1.1;
 constexpr double kBatchLatency = 1e-3;  // launch, H2D of a small batch, D2H, poll
 // A split runs the GPU side's reads beside the pool's hashing on the same
@@ -2343,6 +2820,19 @@ void vx_tuning_stage_huge(vx_ctx* c, int on) {
         if (s.state == Slot::FREE) free_stage(s);
 }
 #endif
+uint64_t vx_tuning_split_take_tail(vx_split* s, uint64_t k) { return s ? split_take_tail(s, k) : 0; }
+size_t vx_tuning_last_split(const vx_ctx* c, double* out, size_t max) {
+    if (!c) return 0;
+    const size_t k = std::min(max, c->last_split.size());
+    for (size_t i = 0; i < k && out; ++i) {
+        const auto& d = c->last_split[i];
+        const double row[12] = {d.t_ms, d.pool_rate, d.engine_rate, d.block_ns, d.t_engine_ms, d.t_pool_ms,
+                                (double)d.unclaimed, (double)d.group, (double)d.lanes, (double)d.pool_done,
+                                (double)d.mode, (double)d.measured};
+        std::memcpy(out + 12 * i, row, sizeof row);
+    }
+    return c->last_split.size();
+}
 size_t vx_tuning_chunk_schedule(uint64_t L, uint64_t C, int head, int tail, uint64_t* out, size_t max) {
     if (C < 4 || C % 4) return 0;
     const auto r = chunk_schedule(L, C, std::max(0, std::min(5, head)), std::max(0, std::min(5, tail)));

@@ -303,6 +303,20 @@ class HashPool:
         shard, vx_verify_files_range); the verdicts then cover that range."""
         return _verify_files(self, paths, file_lengths, piece_length, expected, io_threads, first, count)
 
+    def verify_files_split(self, paths: Sequence[str], file_lengths: Sequence[int], piece_length: int,
+                           expected: bytes, split: "Split", io_threads: int = 0) -> int:
+        """The engine's side of a split re-verify (vx_verify_files_split):
+        verifies the pieces it claims from `split` while the caller's pool
+        claims the others, writes their verdicts into split.matched and
+        returns how many of its pieces hit an I/O error.  Blocks; run the pool
+        on other threads (ctypes drops the GIL for the call)."""
+        arr = (ctypes.c_char_p * max(1, len(paths)))(*[os.fsencode(p) for p in paths])
+        lens = (ctypes.c_uint64 * max(1, len(file_lengths)))(*file_lengths)
+        exp = ctypes.create_string_buffer(bytes(expected), max(1, len(expected)))
+        rc = self.lib.vx_verify_files_split(self._h, arr, lens, len(paths), piece_length, exp, len(expected) // 20,
+                                            ctypes.byref(split.s), split.matched, io_threads)
+        return int(check(rc, "vx_verify_files_split", self.lib))
+
     def verify_batch(self, pieces: Sequence, expected: Sequence[bytes]) -> tuple[list[bool], list[bytes]]:
         n = len(pieces)
         if len(expected) != n:
@@ -333,6 +347,47 @@ def _verify_files(pool: "HashPool", paths: Sequence[str], file_lengths: Sequence
                                          io_threads)
     bad = check(rc, "vx_verify_files", pool.lib)
     return [bool(b) for b in out.raw[:count]], int(bad)
+
+
+class Split:
+    """One bulk re-verify shared at once by the engine and the caller's pool,
+    with no plan (include/vx_hash.h vx_split / vx_verify_files_split): the
+    pool's threads take pieces from the head with claim() and report each
+    finished one with done(); the engine (HashPool.verify_files_split) takes
+    groups from the top, sized from both sides' rates measured as it goes.
+    `matched` holds every verdict once both sides have returned: entries
+    [0, boundary - first) are the pool's to write, the rest the engine's.
+    claim_fn / done_fn / arg are the C addresses a native pool calls."""
+
+    def __init__(self, first: int, end: int, cpu_threads: int = 0, cpu_thread_rate: float = 0.0):
+        self.lib = lib()
+        self.s = _lib.vx_split()
+        check(self.lib.vx_split_init(ctypes.byref(self.s), first, end, cpu_threads, cpu_thread_rate),
+              "vx_split_init", self.lib)
+        self.first, self.end = first, end
+        self.matched = ctypes.create_string_buffer(max(1, end - first))
+        self.arg = ctypes.addressof(self.s)
+        self.claim_fn = ctypes.cast(self.lib.vx_split_claim, ctypes.c_void_p).value
+        self.done_fn = ctypes.cast(self.lib.vx_split_done, ctypes.c_void_p).value
+
+    def claim(self) -> int:
+        """The next piece for the pool, or -1 when none is left."""
+        return int(self.lib.vx_split_claim(ctypes.byref(self.s)))
+
+    def done(self, pieces: int = 1) -> None:
+        self.lib.vx_split_done(ctypes.byref(self.s), pieces)
+
+    @property
+    def boundary(self) -> int:
+        """The engine's lowest piece (end when it took none)."""
+        return int(self.lib.vx_split_boundary(ctypes.byref(self.s)))
+
+    @property
+    def pool_done(self) -> int:
+        return int(self.s.pool_done)
+
+    def verdicts(self) -> list[bool]:
+        return [bool(b) for b in self.matched.raw[:self.end - self.first]]
 
 
 def verify_files_multi(pools: Sequence["HashPool"], paths: Sequence[str], file_lengths: Sequence[int],
