@@ -337,7 +337,8 @@ typedef struct vx_split {
     uint64_t word;          /* head (low 32 bits) | stop (high 32): [head, stop) is unclaimed          */
     uint64_t pool_done;     /* pieces the pool finished (vx_split_done)                                */
     uint64_t start_ns;      /* steady clock at vx_split_init: the pool's rate is measured from here     */
-    uint64_t first, end;    /* the range                                                               */
+    uint64_t first;         /* the range [first, end)                                                  */
+    uint64_t end;
     uint32_t cpu_threads;   /* the pool's threads (0 = no pool: the engine takes every piece)          */
     uint32_t _pad;
     double cpu_thread_rate; /* the pool's bytes/s per thread alone (cold start only; 0 = 2.2e9, SHA-NI) */

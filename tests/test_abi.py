@@ -565,3 +565,59 @@ def test_plan_verify_decisions_on_the_round5_grid(built):
             assert p.use_gpu == (pt["winner"] == "gpu"), pt
         if pt["n"] <= 256:  # chain-bound: one lane's chain, whatever the host
             assert abs(p.gpu_s / pt["gpu_s"] - 1) < 0.10, (pt, p.gpu_s)
+
+
+def _split_scan(n, pl, total, threads, rate, g):
+    """Every split point scored by the model of DESIGN.md §6.6 (the scan the
+    engine replaced with a bisection): the GPU side at 0.74 of the
+    link beside the pool, the pool at 0.80 of its rate beside the engine."""
+    import math
+
+    chain_block, pcie, setup, loss, margin = 0.76e-6, 52.0 * (1 << 30), 1.5e-3, 0.08, 1.1
+    last = total - (n - 1) * pl if n else 0
+
+    def gpu(k):
+        b = (k - 1) * pl + last
+        ch = math.ceil((pl + 9) / 64) * chain_block
+        tr = b / (pcie * (0.74 if k < n else 1.0)) / max(1, g)
+        return max(tr, ch) + setup + loss * min(tr, ch)
+
+    def cpu(k):
+        if k >= n:
+            return 0.0
+        return math.ceil((n - k) / threads) * (pl / (rate * 0.80 if k else rate))
+
+    best_k, best_t = 0, cpu(0)
+    for k in range(1, n + 1):
+        t = max(gpu(k), cpu(k))
+        if t < best_t:
+            best_k, best_t = k, t
+    if best_k and best_t * margin >= cpu(0):
+        best_k = 0
+    return best_k
+
+
+@pytest.mark.parametrize("n,pl,threads,rate,g", [(1387, 2 << 20, 12, 2.32e9, 1), (1387, 2 << 20, 16, 2.2e9, 1),
+                                                 (11093, 256 << 10, 64, 2.2e9, 1), (4000, 1 << 20, 8, 1.5e9, 2),
+                                                 (20000, 16 << 10, 16, 2.2e9, 1), (700, 8 << 20, 24, 2.0e9, 4),
+                                                 (1387, 2 << 20, 128, 2.2e9, 8), (2, 4 << 20, 1, 2.0e9, 1)])
+def test_plan_verify_split_bisection_matches_scan(built, n, pl, threads, rate, g):
+    """The bisected planner picks the point the exhaustive scan of the same
+    model picks (the last piece shorter, so the sides' times are not
+    symmetric)."""
+    total = n * pl - pl // 3
+    first, count, _ = _split(n, pl, total, threads, rate=rate, g=g)
+    assert count == _split_scan(n, pl, total, threads, rate, g), (first, count)
+
+
+def test_plan_verify_split_is_fast_on_huge_torrents(built):
+    """A multi-TB torrent of 16 KiB pieces (10^8 pieces): the planner answers
+    in well under a millisecond per call (it used to score every split point)."""
+    import time
+
+    n, pl = 100_000_000, 16 << 10
+    t0 = time.perf_counter()
+    for _ in range(10):
+        first, count, p = _split(n, pl, n * pl, 16)
+    assert (time.perf_counter() - t0) / 10 < 0.005
+    assert first + count == n

@@ -19,6 +19,7 @@ RUST_TO_C = {
     "usize": "size_t", "c_int": "int", "c_char": "char", "c_void": "void", "f64": "double",
     "VxCtx": "vx_ctx", "VxConfig": "vx_config", "VxCompletion": "vx_completion", "VxPlan": "vx_plan",
     "VxStats": "vx_stats", "VxVerifyTrace": "vx_verify_trace", "VxVerifyRound": "vx_verify_round",
+    "VxSplit": "vx_split",
 }
 
 
@@ -141,7 +142,7 @@ def test_rust_structs_match_header():
     c = c_structs()
     r = rust_structs()
     pairs = {"VxCompletion": "vx_completion", "VxConfig": "vx_config", "VxPlan": "vx_plan", "VxStats": "vx_stats",
-             "VxVerifyTrace": "vx_verify_trace", "VxVerifyRound": "vx_verify_round"}
+             "VxVerifyTrace": "vx_verify_trace", "VxVerifyRound": "vx_verify_round", "VxSplit": "vx_split"}
     for rname, cname in pairs.items():
         assert r[rname] == c[cname], f"{rname} vs {cname}: {r[rname]} / {c[cname]}"
     assert r["VxCtx"] == [("_private", "uint8_t[0]")]  # opaque handle

@@ -217,6 +217,11 @@ struct vx_ctx {
         uint32_t mode, measured;
     };
     std::vector<SplitDecision> last_split;
+    // What earlier split calls measured (a running mean over calls, each call
+    // weighted 1/2), the next call's cold start: the engine's copy intake
+    // (B/s, first copy start to last copy end), the kernel's chain per block,
+    // and the pool's bytes/s per thread beside the engine (0 = none yet).
+    double split_rin = 0, split_bns = 0, split_pool_thread_rate = 0;
     // The file re-verify's chunk rounds put every H2D on this one stream (high
     // priority: its own hardware queue) and only kernels on the slot streams,
     // so no copy ever sits behind a kernel.  Created on first
@@ -1756,15 +1761,20 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
         bool ramp;  // joined in the first round: chunks C/4, C/4, C/2, then C
     };
     std::vector<Lane> act;  // claimed pieces with chunks left, in join order
-    // The first group's head ramp (verify_chunked's, per lane): its first
-    // round is a C/4 chain and a quarter of the bytes, so the call's first
-    // read and the copy that nothing overlaps are short.  Later groups join
-    // rounds whose chain is C anyway, and a ramp would only add rounds.
+    // verify_chunked's ramps (chunk_schedule, depth 1), per lane.  Head: the
+    // first group's first round is a C/4 chain and a quarter of the bytes, so
+    // the call's first read and the copy that nothing overlaps are short
+    // (later groups join rounds whose chain is C anyway).  Tail, every lane:
+    // its last C bytes go as C/2, C/4, rest, so the chain left after the
+    // call's last copy is C/4's, not C's.
     const bool ramp_ok = C >= 4 * vx_files::DirectIo::kBlock;
-    auto chunk_len = [&](uint64_t L, uint64_t a, bool ramp) {
-        uint64_t k = C;
-        if (ramp && ramp_ok && L >= 2 * C) k = a < C / 2 ? C / 4 : a < C ? C / 2 : C;
-        return std::min<uint64_t>(k, L - a);
+    auto chunk_len = [&](uint64_t L, uint64_t a, bool head) {
+        if (!ramp_ok || L < 2 * C) return std::min<uint64_t>(C, L - a);
+        const uint64_t q = C / 4, tail_from = (L - C + q - 1) / q * q;
+        if (head && a < C) return a < C / 2 ? q : C / 2;
+        if (a < tail_from) return std::min<uint64_t>(C, tail_from - a);
+        const uint64_t off = a - tail_from;
+        return off == 0 ? std::min<uint64_t>(C / 2, L - a) : off == C / 2 ? std::min<uint64_t>(q, L - a) : L - a;
     };
     // chunk lengths of a full-length piece joining now (ramped or not)
     auto schedule = [&](bool ramp) {
@@ -1793,7 +1803,10 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
     };
     std::vector<Sent> sent;
     size_t timed = 0, measured_upto = 0;  // rounds [0, measured_upto) are in the rates below
-    double copy_bytes = 0, copy_ms = 0;   // measured copies
+    // The copy intake so far: bytes copied over first copy start -> last copy
+    // end (a copy that waited for its reads counts the wait).
+    double in_bytes = 0, in_ms = 0, in_n = 0;
+    float first_cs = -1;
     std::vector<double> block_ns;         // measured chain per 64-byte block, one per round
     std::vector<uint64_t> timed_bytes;
     std::vector<vx_verify_round> tl;
@@ -1807,11 +1820,17 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
     auto rel_ms = [&](uint64_t t_ns) { return t_ns ? ((double)t_ns - (double)c->verify_t0_ns) * 1e-6 : 0.0; };
     auto consume = [&] { fv.consume(); };
     const double pool_threads = sp->cpu_threads;
-    const double pool_rate0 = pool_threads * (sp->cpu_thread_rate > 0 ? sp->cpu_thread_rate : 2.2e9) / (double)pl;
+    std::vector<std::pair<uint64_t, uint64_t>> pool_samples;  // (steady ns, pool_done) at each decision
+    constexpr uint64_t kPoolWindowNs = 4000000;              // the pool's pace: its last 4 ms
+    const double thread_rate0 = c->split_pool_thread_rate > 0 ? c->split_pool_thread_rate
+                                : sp->cpu_thread_rate > 0    ? sp->cpu_thread_rate
+                                                             : 2.2e9;
+    const double pool_rate0 = pool_threads * thread_rate0 / (double)pl;
+    double last_p = 0;  // the pool's pace at the last decision
 
     // Fold newly finished rounds into the copy and chain rates (events are
     // queried, never waited for).
-    size_t copied_upto = 0;  // rounds whose copy is in copy_bytes / copy_ms
+    size_t copied_upto = 0;  // rounds whose copy is in the intake above
     auto measure = [&] {
         // copies as soon as they end (the first rate arrives a kernel earlier)
         while (copied_upto < sent.size()) {
@@ -1819,10 +1838,13 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             if (r.ev >= 0) {
                 const size_t e = 3 * (size_t)r.ev;
                 if (hipEventQuery(c->copy_ev[e + 1]) != hipSuccess) break;
-                float cm = 0;
-                if (hipEventElapsedTime(&cm, c->copy_ev[e], c->copy_ev[e + 1]) == hipSuccess && cm > 0) {
-                    copy_bytes += (double)r.bytes;
-                    copy_ms += cm;
+                float cs = 0, ce = 0;
+                if (hipEventElapsedTime(&cs, c->copy_ev[0], c->copy_ev[e]) == hipSuccess &&
+                    hipEventElapsedTime(&ce, c->copy_ev[0], c->copy_ev[e + 1]) == hipSuccess) {
+                    if (first_cs < 0) first_cs = cs;
+                    in_bytes += (double)r.bytes;
+                    in_ms = (double)ce - (double)first_cs;
+                    in_n += 1;
                 }
             }
             ++copied_upto;
@@ -1866,21 +1888,42 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
         const uint64_t unclaimed = stop > head ? stop - head : 0;
         if (unclaimed == 0 || room == 0) return 0;
         const uint64_t done = __atomic_load_n(&sp->pool_done, __ATOMIC_ACQUIRE);
-        const double el = ((double)vx_files::Readers::now_ns() - (double)sp->start_ns) * 1e-9;
+        const uint64_t now = vx_files::Readers::now_ns();
+        const double el = ((double)now - (double)sp->start_ns) * 1e-9;
         const bool pool_measured = pool_threads == 0 || (done >= std::max(4.0, pool_threads) && el > 0);
-        const double p = pool_threads == 0 ? 0.0 : pool_measured ? (double)done / el : pool_rate0;
-        const double in_hand = (double)(head - first) - (double)std::min<uint64_t>(done, head - first);
+        // The pool's rate over the last few ms (its start-up — threads
+        // spawning, first pieces — is not its pace), or since the start.
+        double p = pool_threads == 0 ? 0.0 : pool_measured ? (double)done / el : pool_rate0;
+        bool windowed = pool_threads == 0;
+        for (size_t k = pool_samples.size(); pool_measured && pool_threads > 0 && k-- > 0;) {
+            const auto& sm = pool_samples[k];
+            if (now - sm.first >= kPoolWindowNs) {
+                if (done > sm.second) p = (double)(done - sm.second) / ((double)(now - sm.first) * 1e-9);
+                windowed = done > sm.second;
+                break;
+            }
+        }
+        pool_samples.emplace_back(now, done);
+        // The first group is decided before the pool has a pace: a rate since
+        // the start is mostly its start-up, so it never goes below the rate the
+        // caller measured alone (an over-claim cannot be handed back; an
+        // under-claim is topped up once the rates are in).
+        if (mode == 1 && pool_threads > 0) p = std::max(p, pool_rate0);
+        // pieces the pool holds count half done
+        const double in_hand = 0.5 * ((double)(head - first) - (double)std::min<uint64_t>(done, head - first));
         // The engine counts as measured once one copy is timed: its chain per
         // block is a property of the kernel, known within a few % before any
         // round of this call ends (kChainBlock), and waiting for a kernel end
         // put the first measured group a whole round later.
-        *measured = copy_ms > 0 && pool_measured;
+        // A later group needs the pool's pace over a window (not its start-up)
+        // and the engine's intake over two copies.
+        *measured = in_n >= 2 && windowed;
         if (!*measured && mode == 0) return 0;
-        // engine rates
-        double rin = copy_ms > 0 ? copy_bytes / (copy_ms * 1e-3) : kPcieRate;
-        if (rd.busy_ns() > 0 && rd.threads() > 0)
-            rin = std::min(rin, (double)rd.bytes_read() / ((double)rd.busy_ns() * 1e-9 / (double)rd.threads()));
-        double bns = kChainBlock * 1e9;
+        if (windowed) last_p = p;
+        const double rin = in_n >= 2 && in_ms > 0 ? in_bytes / (in_ms * 1e-3)
+                           : c->split_rin > 0     ? c->split_rin
+                                                  : kPcieRate;
+        double bns = c->split_bns > 0 ? c->split_bns : kChainBlock * 1e9;
         if (!block_ns.empty()) {
             std::vector<double> b = block_ns;
             std::nth_element(b.begin(), b.begin() + b.size() / 2, b.end());
@@ -1889,10 +1932,13 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
         auto round_s = [&](double bytes, uint64_t chunk) {
             return std::max(bytes / rin, (double)((chunk + 63) / 64) * bns * 1e-9);
         };
-        // rounds queued ahead of the new group (formed, or enqueued and not measured)
+        // rounds queued ahead of the new group (enqueued and not finished, or
+        // formed), in order; nothing sent yet: the first round's read too
         double t_queued = 0;
-        for (const Round& r : formed) t_queued += round_s((double)r.bytes, r.max_chunk);
-        for (size_t k = measured_upto; k < sent.size(); ++k) t_queued += round_s((double)sent[k].bytes, sent[k].max_chunk);
+        uint64_t last_k = 0;  // the longest chunk of the last round queued
+        for (size_t k = measured_upto; k < sent.size(); ++k)
+            t_queued += round_s((double)sent[k].bytes, sent[k].max_chunk), last_k = sent[k].max_chunk;
+        for (const Round& r : formed) t_queued += round_s((double)r.bytes, r.max_chunk), last_k = r.max_chunk;
         // future rounds of the active lanes: bytes per round index
         std::vector<double> fut;
         std::vector<uint64_t> fut_max;  // each future round's longest chunk
@@ -1908,20 +1954,30 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             }
         }
         const std::vector<uint64_t>& js = mode == 1 ? sched_ramp : sched_plain;
+        // Each round costs max(its bytes over the intake, its chain), copies
+        // overlapping the previous round's kernel; after the last copy, the
+        // last kernel's chain; before the first, the first round's read.
+        const bool first_read = sent.empty() && formed.empty();
         auto t_engine = [&](uint64_t j) {
             double t = t_queued;
+            uint64_t k_end = last_k;
             const size_t R = std::max<size_t>(fut.size(), j ? js.size() : 0);
             for (size_t r = 0; r < R; ++r) {
                 double b = r < fut.size() ? fut[r] : 0.0;
                 uint64_t k = r < fut_max.size() ? fut_max[r] : 0;
                 if (j && r < js.size()) b += (double)j * (double)js[r], k = std::max(k, js[r]);
-                if (b > 0) t += round_s(b, k);
+                if (b > 0) t += round_s(b, k) + (r == 0 && first_read ? b / rin : 0.0), k_end = k;
             }
-            return t;
+            return t + (double)((k_end + 63) / 64) * bns * 1e-9;
         };
         auto t_pool = [&](uint64_t j) {
             return p > 0 ? ((double)(unclaimed - j) + in_hand) / p : std::numeric_limits<double>::infinity();
         };
+        // A later group rides the rounds the active lanes still have; one that
+        // needs more than one round beyond them adds a tail of rounds that are
+        // one chain each with PCIe idle, which a rate misread from a short
+        // window (a host-wide stall slows both sides for 10+ ms) cannot repay.
+        if (mode == 0 && !act.empty() && js.size() > fut.size() + 1) return 0;
         // the largest j in [0, min(unclaimed, room)] with t_engine(j) <= t_pool(j):
         // t_engine grows with j and t_pool shrinks, so bisect
         auto ok = [&](uint64_t j) { return t_engine(j) <= t_pool(j); };
@@ -1936,6 +1992,10 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             }
         }
 
+        // and a later group must shorten the predicted end by a tenth
+        if (mode == 0 && lo > 0 &&
+            std::max(t_engine(lo), t_pool(lo)) > 0.9 * std::max(t_engine(0), t_pool(0)))
+            lo = 0;
         c->last_split.push_back(vx_ctx::SplitDecision{
             ((double)vx_files::Readers::now_ns() - (double)c->verify_t0_ns) * 1e-6, p, rin, bns,
             t_engine(lo) * 1e3, t_pool(lo) * 1e3, unclaimed, lo, (uint64_t)act.size(), done, (uint32_t)mode,
@@ -2101,9 +2161,20 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
         }
     }
     c->last_rounds = std::move(tl);
-    if (!rc)
+    if (!rc) {
         for (uint64_t i = lo_row; i < cnt; ++i)
             if (fv.bad[i]) fv.matched_out[i] = 0;
+        // the next split call's cold start (this host, this load): each
+        // call's whole-call figures, averaged with the earlier calls' at 1/2
+        measure();
+        auto mean = [](double& m, double v) { m = m > 0 ? 0.5 * (m + v) : v; };
+        if (in_n >= 2 && in_ms > 0) mean(c->split_rin, in_bytes / (in_ms * 1e-3));
+        if (!block_ns.empty()) {
+            std::nth_element(block_ns.begin(), block_ns.begin() + block_ns.size() / 2, block_ns.end());
+            mean(c->split_bns, block_ns[block_ns.size() / 2]);
+        }
+        if (last_p > 0 && pool_threads > 0) mean(c->split_pool_thread_rate, last_p * (double)pl / pool_threads);
+    }
     fv.done = cnt - lo_row;
     return rc;
 }
@@ -2738,14 +2809,44 @@ int vx_plan_verify_split(uint64_t n_pieces, uint32_t piece_length, uint64_t tota
         return std::ceil((double)(n_pieces - k) / threads) * (L / (k ? rate * kSplitPool : rate));
     };
     vx_plan g{};
+    auto gpu_time = [&](uint64_t k) {
+        plan_gpu(L, gpu_bytes(k), n_gpus, &g, k < n_pieces ? kSplitLink : 1.0);
+        return g.gpu_s;
+    };
     uint64_t best_k = 0;
     double best_t = cpu_time(0);
     const double pool_alone = best_t;
-    for (uint64_t k = 1; k <= n_pieces; ++k) {
-        plan_gpu(L, gpu_bytes(k), n_gpus, &g, k < n_pieces ? kSplitLink : 1.0);
-        const double t = std::max(g.gpu_s, cpu_time(k));
-        if (t < best_t) best_t = t, best_k = k;
+    auto consider = [&](uint64_t k) {
+        if (k < 1 || k > n_pieces) return;
+        const double t = std::max(gpu_time(k), cpu_time(k));
+        if (t < best_t || (t == best_t && k < best_k)) best_t = t, best_k = k;
+    };
+    // On 1 <= k < n the GPU side's time never falls as k grows and the
+    // pool's never rises, so the slower side is least where they cross:
+    // bisect for the first k whose GPU time reaches the pool's, then score it,
+    // its neighbours and k = n (whose link has no pool beside it).  A scan of
+    // every k cost a multi-TB torrent of 16 KiB pieces ~10^7 evaluations.
+    if (n_pieces > 1) {
+        uint64_t lo = 1, hi = n_pieces - 1;
+        if (gpu_time(hi) < cpu_time(hi)) {
+            lo = hi;
+        } else {
+            while (lo < hi) {
+                const uint64_t mid = lo + (hi - lo) / 2;
+                if (gpu_time(mid) >= cpu_time(mid)) hi = mid;
+                else lo = mid + 1;
+            }
+        }
+        for (uint64_t k = lo > 2 ? lo - 2 : 1; k <= std::min<uint64_t>(n_pieces - 1, lo + 2); ++k) consider(k);
+        // left of the crossing the pool's side binds, and its time is a step
+        // function (rounds of `threads` pieces): the step's first k ties it
+        if (lo > 1) {
+            const uint64_t m = (uint64_t)std::ceil((double)(n_pieces - (lo - 1)) / threads);
+            const uint64_t k0 = n_pieces > m * (uint64_t)threads ? n_pieces - m * (uint64_t)threads : 1;
+            consider(std::max<uint64_t>(1, k0));
+        }
     }
+    consider(n_pieces);
     if (best_k && best_t * kMargin >= pool_alone) best_k = 0;
     *gpu_count = best_k;
     *gpu_first = n_pieces - best_k;
