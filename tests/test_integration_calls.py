@@ -314,7 +314,8 @@ def test_call_sites_type_check():
     assert not problems, "\n".join(problems)
     called = {name for _, name, _, _ in ck.calls()}
     for must in ("vx_create", "vx_submit", "vx_submit_piece", "vx_set_piece_table", "vx_flush", "vx_poll",
-                 "vx_verify_files", "vx_verify_files_multi", "vx_plan_verify", "vx_plan_verify_split",
+                 "vx_verify_files", "vx_verify_files_multi", "vx_plan_verify", "vx_verify_files_split",
+                 "vx_split_init", "vx_split_claim", "vx_split_done", "vx_split_boundary",
                  "vx_register_host_buffer",
                  "vx_destroy", "spawn", "drain_into"):
         assert must in called, must

@@ -9,7 +9,9 @@ it records wall / engine / pool seconds, the boundary, every round's decision
 (vx_tuning_last_split: rates, predicted remaining times, the group taken) and
 the round timeline's GPU kernel ends, to JSON.
 
-usage: python tools/split_probe.py OUT.json [reps] [pool_threads] [readers]
+usage: python tools/split_probe.py OUT.json [reps] [pool_threads] [readers] [sweep]
+  sweep: comma-separated scales of the planner's GPU share for the fixed
+  points (default 1.0: the planner's point only)
 """
 import ctypes
 import json
@@ -41,9 +43,11 @@ def main():
     threads = bench.cpu_share()
     pool_t = int(sys.argv[3]) if len(sys.argv) > 3 else max(1, threads * 3 // 4)
     io_t = int(sys.argv[4]) if len(sys.argv) > 4 else max(2, threads // 2)
+    sweep = [float(x) for x in sys.argv[5].split(",")] if len(sys.argv) > 5 else [1.0]
     pl = 2097152
     path = os.path.join(bench.reverify_dir(), f"vx_split_probe_{os.getpid()}.iso")
     res = {"pool_threads": pool_t, "readers": io_t, "calls": [], "fixed": []}
+    summary_b = []
     try:
         total, n, last = bench.write_linuxmint_file(path)
         exp = oracle.pool_digest_synth(0x5EED0005, 0, n, pl, last_index=n - 1, last_len=last, threads=threads)
@@ -67,15 +71,24 @@ def main():
                                                  "ce": round(x["copy_end_ms"], 2), "ke": round(x["kernel_end_ms"], 2),
                                                  "mb": round(x["bytes"] / 1e6, 1), "lanes": x["lanes"]}
                                                 for x in rounds]})
-                f = bench.split_call(pool, [path], [total], n, pl, exp, plan["gpu_first"], io_t, pool_t)
-                res["fixed"].append({"s": round(f["s"], 4), "gpu_s": round(f["gpu_s"], 4),
-                                     "cpu_s": round(f["cpu_s"], 4)})
+                summary_b.append(c["s"])
+                k0 = n - plan["gpu_first"]
+                fixed = {}
+                for scale in sweep:  # fixed points: the planner's GPU share scaled
+                    first = max(0, min(n, n - int(round(k0 * scale))))
+                    f = bench.split_call(pool, [path], [total], n, pl, exp, first, io_t, pool_t)
+                    fixed[first] = round(f["s"], 4)
+                res["fixed"].append(fixed)
                 print(f"rep {r}: balanced {c['s'] * 1e3:.1f} ms (gpu {c['gpu_s'] * 1e3:.1f}, pool "
-                      f"{c['cpu_s'] * 1e3:.1f}, boundary {c['boundary']}); fixed@{plan['gpu_first']} "
-                      f"{f['s'] * 1e3:.1f} ms (gpu {f['gpu_s'] * 1e3:.1f}, pool {f['cpu_s'] * 1e3:.1f})", flush=True)
+                      f"{c['cpu_s'] * 1e3:.1f}, boundary {c['boundary']}); fixed "
+                      + " ".join(f"@{k}:{v * 1e3:.1f}" for k, v in fixed.items()), flush=True)
     finally:
         if os.path.exists(path):
             os.unlink(path)
+    med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+    res["balanced_median_s"] = med(summary_b)
+    res["fixed_median_s"] = {k: med([f[k] for f in res["fixed"] if k in f]) for k in res["fixed"][0]}
+    print("median: balanced", res["balanced_median_s"], "fixed", res["fixed_median_s"], flush=True)
     with open(out, "w") as fo:
         json.dump(res, fo, indent=1)
 
