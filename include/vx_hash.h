@@ -362,7 +362,8 @@ uint64_t vx_split_boundary(const vx_split* s);
  * pieces' entries, the pool writes the others.  Returns the number of the
  * engine's pieces that hit an I/O error (>= 0), or a VX_E* code: then the
  * pieces [vx_split_boundary(s), end) have no verdict and the caller verifies
- * them itself.  Requires no async pieces pending on ctx.  vx_last_verify and
+ * them itself.  One engine per split: a second vx_verify_files_split on the
+ * same vx_split fails with VX_EINVAL.  Requires no async pieces pending on ctx.  vx_last_verify and
  * vx_last_verify_rounds describe the call as for vx_verify_files. */
 int64_t vx_verify_files_split(vx_ctx* ctx, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
                               uint32_t piece_length, const uint8_t* expected, size_t n_pieces, vx_split* s,

@@ -145,3 +145,32 @@ def test_split_engine_failure_leaves_its_pieces_to_the_caller(built, gpu, tmp_pa
         # the same context, next call: a clean split
         sp, taken, bad = _run_split(pool, paths, sizes, pl, exp, 0, n, 2)
         assert sp.verdicts() == want and bad == 0
+
+
+def test_split_refuses_a_second_engine(built, gpu, tmp_path):
+    """One engine per split (vx_hash.h): two contexts racing on one vx_split
+    — the first to claim keeps the split, the other fails with VX_EINVAL
+    before claiming anything, so every verdict still comes from one side."""
+    from vortex_amd._lib import VX_EINVAL, VxError
+    from vortex_amd.hash_pool import HashPool, Split
+
+    pl, n = 1 << 20, 64
+    paths, sizes, exp = _files(tmp_path, pl, [n * pl - 999], 17)
+    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
+    sp = Split(0, n, 0)
+    out = {}
+    with HashPool(pl, slots=3, slot_bytes=64 << 20) as a, HashPool(pl, slots=3, slot_bytes=64 << 20) as b:
+        def run(name, pool):
+            try:
+                out[name] = pool.verify_files_split(paths, sizes, pl, exp, sp, io_threads=2)
+            except VxError as e:
+                out[name] = e
+
+        ths = [threading.Thread(target=run, args=(k, p)) for k, p in (("a", a), ("b", b))]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+    errs = [v for v in out.values() if isinstance(v, VxError)]
+    assert len(errs) == 1 and errs[0].code == VX_EINVAL, out
+    assert sp.boundary == 0 and sp.verdicts() == want

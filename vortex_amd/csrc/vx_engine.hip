@@ -1712,10 +1712,13 @@ constexpr double kChainBlock = 0.76e-6, kPcieRate = 52.0 * (1ull << 30);
 // up one piece per compare-and-swap (vx_split_claim); the engine moves stop
 // down by a group (split_take_tail).  Neither side can take a piece the other
 // has, and a group the engine asks for is cut to what is still unclaimed.
-uint64_t split_take_tail(vx_split* s, uint64_t k) {
+// expect: the stop this engine left (UINT64_MAX: any); a different stop means
+// a second engine claims from the same split, and the call returns UINT64_MAX.
+uint64_t split_take_tail(vx_split* s, uint64_t k, uint64_t expect = UINT64_MAX) {
     uint64_t w = __atomic_load_n(&s->word, __ATOMIC_ACQUIRE);
     for (;;) {
         const uint64_t head = w & 0xffffffffull, stop = w >> 32;
+        if (expect != UINT64_MAX && stop != expect) return UINT64_MAX;
         const uint64_t take = std::min(k, stop > head ? stop - head : 0);
         if (take == 0) return stop;
         const uint64_t nw = head | ((stop - take) << 32);
@@ -2036,7 +2039,11 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
                 const bool continues = !act.empty();
                 if (j) {
                     const uint64_t old = *lowest;  // the engine alone lowers stop: it is still here
-                    const uint64_t lo = split_take_tail(sp, j);
+                    const uint64_t lo = split_take_tail(sp, j, old);
+                    if (lo == UINT64_MAX) {
+                        rc = fail(VX_EINVAL, "vx_verify_files_split: another engine claims from this split");
+                        return -1;
+                    }
                     for (uint64_t i = lo; i < old; ++i) lanes.push_back(Lane{i, 0, !formed_any});
                     *lowest = std::min(*lowest, lo);
                 }
