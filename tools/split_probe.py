@@ -9,9 +9,10 @@ it records wall / engine / pool seconds, the boundary, every round's decision
 (vx_tuning_last_split: rates, predicted remaining times, the group taken) and
 the round timeline's GPU kernel ends, to JSON.
 
-usage: python tools/split_probe.py OUT.json [reps] [pool_threads] [readers] [sweep]
+usage: python tools/split_probe.py OUT.json [reps] [pool_threads] [readers] [sweep] [cold]
   sweep: comma-separated scales of the planner's GPU share for the fixed
-  points (default 1.0: the planner's point only)
+  points (default 1.0: the planner's point only); "cold" evicts the file
+  (fsync + POSIX_FADV_DONTNEED) before every call
 """
 import ctypes
 import json
@@ -44,6 +45,7 @@ def main():
     pool_t = int(sys.argv[3]) if len(sys.argv) > 3 else max(1, threads * 3 // 4)
     io_t = int(sys.argv[4]) if len(sys.argv) > 4 else max(2, threads // 2)
     sweep = [float(x) for x in sys.argv[5].split(",")] if len(sys.argv) > 5 else [1.0]
+    cold = len(sys.argv) > 6 and sys.argv[6] == "cold"  # evict the file before every call
     pl = 2097152
     path = os.path.join(bench.reverify_dir(), f"vx_split_probe_{os.getpid()}.iso")
     res = {"pool_threads": pool_t, "readers": io_t, "calls": [], "fixed": []}
@@ -61,7 +63,14 @@ def main():
         res["rate_per_thread"] = rate
         with HashPool(pl, slots=4, slot_bytes=512 << 20, batch_pieces=4096, hooks=True) as pool:
             pool.verify_files([path], [total], pl, exp, io_threads=threads)
+            def evict():
+                if cold:
+                    bench.drop_cache(path)
+
+            res["cold"] = cold
+            res["alone"] = []
             for r in range(reps):
+                evict()
                 c = bench.balanced_call(pool, [path], [total], n, pl, exp, io_t, pool_t, rate)
                 rounds = pool.last_verify_rounds()
                 res["calls"].append({"s": round(c["s"], 4), "gpu_s": round(c["gpu_s"], 4),
@@ -76,19 +85,28 @@ def main():
                 fixed = {}
                 for scale in sweep:  # fixed points: the planner's GPU share scaled
                     first = max(0, min(n, n - int(round(k0 * scale))))
+                    evict()
                     f = bench.split_call(pool, [path], [total], n, pl, exp, first, io_t, pool_t)
                     fixed[first] = round(f["s"], 4)
                 res["fixed"].append(fixed)
+                alone = {}
+                for name, first, io_c, pool_c in (("gpu", 0, threads, threads), ("pool", n, threads, threads)):
+                    evict()
+                    alone[name] = round(bench.split_call(pool, [path], [total], n, pl, exp, first, io_c, pool_c)["s"], 4)
+                res["alone"].append(alone)
                 print(f"rep {r}: balanced {c['s'] * 1e3:.1f} ms (gpu {c['gpu_s'] * 1e3:.1f}, pool "
                       f"{c['cpu_s'] * 1e3:.1f}, boundary {c['boundary']}); fixed "
-                      + " ".join(f"@{k}:{v * 1e3:.1f}" for k, v in fixed.items()), flush=True)
+                      + " ".join(f"@{k}:{v * 1e3:.1f}" for k, v in fixed.items())
+                      + f"; alone gpu {alone['gpu'] * 1e3:.1f} pool {alone['pool'] * 1e3:.1f}", flush=True)
     finally:
         if os.path.exists(path):
             os.unlink(path)
     med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
     res["balanced_median_s"] = med(summary_b)
     res["fixed_median_s"] = {k: med([f[k] for f in res["fixed"] if k in f]) for k in res["fixed"][0]}
-    print("median: balanced", res["balanced_median_s"], "fixed", res["fixed_median_s"], flush=True)
+    res["alone_median_s"] = {k: med([a[k] for a in res["alone"]]) for k in ("gpu", "pool")}
+    print("median: balanced", res["balanced_median_s"], "fixed", res["fixed_median_s"], "alone",
+          res["alone_median_s"], flush=True)
     with open(out, "w") as fo:
         json.dump(res, fo, indent=1)
 
