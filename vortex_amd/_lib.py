@@ -46,6 +46,7 @@ EXPORTS = (
     "vx_plan_verify", "vx_plan_verify_gpus", "vx_plan_verify_split", "vx_get_stats", "vx_reset_stats",
     "vx_last_verify", "vx_last_verify_rounds",
     "vx_split_init", "vx_split_claim", "vx_split_done", "vx_split_boundary", "vx_verify_files_split",
+    "vx_verify_files_split_multi",
 )
 # ... plus include/vx_tuning.h and include/vx_synth.h: libvortex_amd_tuning.so only.
 TUNING_EXPORTS = (
@@ -123,7 +124,7 @@ class vx_split(ctypes.Structure):
     """The split's claim word and the pool's progress (include/vx_hash.h)."""
     _fields_ = [("word", ctypes.c_uint64), ("pool_done", ctypes.c_uint64), ("start_ns", ctypes.c_uint64),
                 ("first", ctypes.c_uint64), ("end", ctypes.c_uint64), ("cpu_threads", ctypes.c_uint32),
-                ("_pad", ctypes.c_uint32), ("cpu_thread_rate", ctypes.c_double)]
+                ("engines", ctypes.c_uint32), ("cpu_thread_rate", ctypes.c_double)]
 
 
 _lib = None
@@ -178,6 +179,8 @@ def _declare(L: ctypes.CDLL, tuning: bool = False) -> None:
         "vx_split_boundary": ([c.POINTER(vx_split)], c.c_uint64),
         "vx_verify_files_split": ([vp, vp, vp, c.c_size_t, c.c_uint32, vp, c.c_size_t, c.POINTER(vx_split), vp,
                                    c.c_uint32], c.c_int64),
+        "vx_verify_files_split_multi": ([vp, c.c_size_t, vp, vp, c.c_size_t, c.c_uint32, vp, c.c_size_t,
+                                         c.POINTER(vx_split), vp, c.c_uint32], c.c_int64),
     }
     if tuning:
         sig.update({

@@ -1442,27 +1442,54 @@ struct ChunkPipe {
     // Wait for every round, then copy verdicts / digests back (either may be
     // NULL).  bad (may be NULL): pieces the caller fails for an I/O error,
     // counted in io_errors and not again as mismatches.
-    // Only rows [lo, hi) are the call's (the split: the engine's pieces).
-    int finish(uint8_t* matched_out, uint8_t* digests_out, int rc, const uint8_t* bad = nullptr, uint64_t lo = 0,
-               uint64_t hi = UINT64_MAX) {
-        hi = std::min(hi, cnt);
-        lo = std::min(lo, hi);
+    int finish(uint8_t* matched_out, uint8_t* digests_out, int rc, const uint8_t* bad = nullptr) {
         if (!rc) {
             for (auto& s : c->slots)
                 if (s.state == Slot::INFLIGHT && hipEventSynchronize(s.done) != hipSuccess) rc = VX_EDEVICE;
             if (rc) (void)fail(rc, "chunk rounds failed on device");
         }
-        if (!rc && matched_out && d_match && hi > lo &&
-            hipMemcpy(matched_out + lo, d_match + lo, hi - lo, hipMemcpyDeviceToHost) != hipSuccess)
+        if (!rc && matched_out && d_match && hipMemcpy(matched_out, d_match, cnt, hipMemcpyDeviceToHost) != hipSuccess)
             rc = fail(VX_EDEVICE, "verdict D2H failed");
-        if (!rc && digests_out && hi > lo &&
-            hipMemcpy(digests_out + 20 * lo, d_dig + 20 * lo, (hi - lo) * 20, hipMemcpyDeviceToHost) != hipSuccess)
+        if (!rc && digests_out && hipMemcpy(digests_out, d_dig, cnt * 20, hipMemcpyDeviceToHost) != hipSuccess)
             rc = fail(VX_EDEVICE, "digest D2H failed");
         if (!rc) {
-            c->stats.pieces_completed += hi - lo;
+            c->stats.pieces_completed += cnt;
             c->stats.bytes_completed += bytes;
             if (matched_out && d_match)
-                for (uint64_t i = lo; i < hi; ++i) c->stats.pieces_mismatched += matched_out[i] == 0 && !(bad && bad[i]);
+                for (uint64_t i = 0; i < cnt; ++i) c->stats.pieces_mismatched += matched_out[i] == 0 && !(bad && bad[i]);
+        }
+        for (auto& s : c->slots)
+            if (s.state == Slot::INFLIGHT) {
+                (void)hipEventSynchronize(s.done);
+                reset_fill(s);
+                s.state = Slot::FREE;
+            }
+        return rc;
+    }
+
+    // finish() for a set of row ranges (the split: this engine's claims):
+    // verdicts back for those rows only, and only they count in vx_stats.
+    int finish_rows(uint8_t* matched_out, int rc, const uint8_t* bad,
+                    const std::vector<std::pair<uint64_t, uint64_t>>& rows) {
+        if (!rc) {
+            for (auto& s : c->slots)
+                if (s.state == Slot::INFLIGHT && hipEventSynchronize(s.done) != hipSuccess) rc = VX_EDEVICE;
+            if (rc) (void)fail(rc, "chunk rounds failed on device");
+        }
+        for (const auto& r : rows) {
+            const uint64_t lo = std::min(r.first, cnt), hi = std::min(r.second, cnt);
+            if (!rc && matched_out && d_match && hi > lo &&
+                hipMemcpy(matched_out + lo, d_match + lo, hi - lo, hipMemcpyDeviceToHost) != hipSuccess)
+                rc = fail(VX_EDEVICE, "verdict D2H failed");
+        }
+        if (!rc) {
+            c->stats.bytes_completed += bytes;
+            for (const auto& r : rows) {
+                c->stats.pieces_completed += r.second - r.first;
+                if (matched_out && d_match)
+                    for (uint64_t i = r.first; i < r.second; ++i)
+                        c->stats.pieces_mismatched += matched_out[i] == 0 && !(bad && bad[i]);
+            }
         }
         for (auto& s : c->slots)
             if (s.state == Slot::INFLIGHT) {
@@ -1712,12 +1739,15 @@ constexpr double kChainBlock = 0.76e-6, kPcieRate = 52.0 * (1ull << 30);
 // up one piece per compare-and-swap (vx_split_claim); the engine moves stop
 // down by a group (split_take_tail).  Neither side can take a piece the other
 // has, and a group the engine asks for is cut to what is still unclaimed.
+// The claimed pieces are [returned, *was) (*was: the stop before the claim).
 // expect: the stop this engine left (UINT64_MAX: any); a different stop means
-// a second engine claims from the same split, and the call returns UINT64_MAX.
-uint64_t split_take_tail(vx_split* s, uint64_t k, uint64_t expect = UINT64_MAX) {
+// an engine the split was not declared for (vx_split.engines) claims from it,
+// and the call returns UINT64_MAX.
+uint64_t split_take_tail(vx_split* s, uint64_t k, uint64_t expect = UINT64_MAX, uint64_t* was = nullptr) {
     uint64_t w = __atomic_load_n(&s->word, __ATOMIC_ACQUIRE);
     for (;;) {
         const uint64_t head = w & 0xffffffffull, stop = w >> 32;
+        if (was) *was = stop;
         if (expect != UINT64_MAX && stop != expect) return UINT64_MAX;
         const uint64_t take = std::min(k, stop > head ? stop - head : 0);
         if (take == 0) return stop;
@@ -1823,6 +1853,10 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
     auto rel_ms = [&](uint64_t t_ns) { return t_ns ? ((double)t_ns - (double)c->verify_t0_ns) * 1e-6 : 0.0; };
     auto consume = [&] { fv.consume(); };
     const double pool_threads = sp->cpu_threads;
+    // engines claiming from this split at once (vx_split.engines): each takes
+    // an equal share of what the pool does not
+    const uint64_t engines = std::max<uint32_t>(1, sp->engines);
+    std::vector<std::pair<uint64_t, uint64_t>> mine;  // this engine's claims, [lo, hi), in claim order
     std::vector<std::pair<uint64_t, uint64_t>> pool_samples;  // (steady ns, pool_done) at each decision
     constexpr uint64_t kPoolWindowNs = 4000000;              // the pool's pace: its last 4 ms
     const double thread_rate0 = c->split_pool_thread_rate > 0 ? c->split_pool_thread_rate
@@ -1973,8 +2007,9 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             }
             return t + (double)((k_end + 63) / 64) * bns * 1e-9;
         };
-        auto t_pool = [&](uint64_t j) {
-            return p > 0 ? ((double)(unclaimed - j) + in_hand) / p : std::numeric_limits<double>::infinity();
+        auto t_pool = [&](uint64_t j) {  // the others take an equal share each
+            const double left = (double)unclaimed - (double)(engines * j);
+            return p > 0 ? (std::max(0.0, left) + in_hand) / p : std::numeric_limits<double>::infinity();
         };
         // A later group rides the rounds the active lanes still have; one that
         // needs more than one round beyond them adds a tail of rounds that are
@@ -1984,7 +2019,7 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
         // the largest j in [0, min(unclaimed, room)] with t_engine(j) <= t_pool(j):
         // t_engine grows with j and t_pool shrinks, so bisect
         auto ok = [&](uint64_t j) { return t_engine(j) <= t_pool(j); };
-        uint64_t lo = 0, hi = std::min(unclaimed, room);
+        uint64_t lo = 0, hi = std::min(engines == 1 ? unclaimed : (unclaimed + engines - 1) / engines, room);
         if (ok(hi)) {
             lo = hi;
         } else if (ok(1)) {
@@ -2038,12 +2073,14 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
                 std::vector<Lane> lanes = act;
                 const bool continues = !act.empty();
                 if (j) {
-                    const uint64_t old = *lowest;  // the engine alone lowers stop: it is still here
-                    const uint64_t lo = split_take_tail(sp, j, old);
+                    // alone on the split, the stop is where this engine left it
+                    uint64_t old = 0;
+                    const uint64_t lo = split_take_tail(sp, j, engines == 1 ? *lowest : UINT64_MAX, &old);
                     if (lo == UINT64_MAX) {
                         rc = fail(VX_EINVAL, "vx_verify_files_split: another engine claims from this split");
                         return -1;
                     }
+                    if (lo < old) mine.emplace_back(lo, old);
                     for (uint64_t i = lo; i < old; ++i) lanes.push_back(Lane{i, 0, !formed_any});
                     *lowest = std::min(*lowest, lo);
                 }
@@ -2141,9 +2178,13 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             reset_fill(sl);
             sl.state = Slot::FREE;
         }
-    const uint64_t lo_row = *lowest - first;
-    for (uint64_t i = *lowest; i < end; ++i) cp.bytes += plen(i);
-    rc = cp.finish(fv.matched_out, nullptr, rc, fv.bad.data(), lo_row, cnt);
+    // rows of this engine's pieces, relative to first
+    std::vector<std::pair<uint64_t, uint64_t>> rows;
+    for (const auto& r : mine) {
+        rows.emplace_back(r.first - first, r.second - first);
+        for (uint64_t i = r.first; i < r.second; ++i) cp.bytes += plen(i);
+    }
+    rc = cp.finish_rows(fv.matched_out, rc, fv.bad.data(), rows);
     vx_verify_trace& vt = c->last_verify;
     vt.tail_ms = std::chrono::duration<double, std::milli>(clk::now() - t_last_enqueue).count();
     if (!rc && timed) {
@@ -2169,8 +2210,9 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
     }
     c->last_rounds = std::move(tl);
     if (!rc) {
-        for (uint64_t i = lo_row; i < cnt; ++i)
-            if (fv.bad[i]) fv.matched_out[i] = 0;
+        for (const auto& r : rows)
+            for (uint64_t i = r.first; i < r.second; ++i)
+                if (fv.bad[i]) fv.matched_out[i] = 0;
         // the next split call's cold start (this host, this load): each
         // call's whole-call figures, averaged with the earlier calls' at 1/2
         measure();
@@ -2182,7 +2224,8 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
         }
         if (last_p > 0 && pool_threads > 0) mean(c->split_pool_thread_rate, last_p * (double)pl / pool_threads);
     }
-    fv.done = cnt - lo_row;
+    fv.done = 0;
+    for (const auto& r : rows) fv.done += r.second - r.first;
     return rc;
 }
 
@@ -2519,7 +2562,7 @@ static int64_t verify_files_impl(vx_ctx* c, const char* const* paths, const uint
         rc = sp        ? verify_split(fv, rd, sp, n_pieces, piece_length, total, Cv, &lowest)
              : chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total, first, end, Cv)
                        : verify_whole(fv, rd, n_pieces, piece_length, total, first, end);
-        if (sp) std::fill(bad.begin(), bad.begin() + (lowest - first), 0);  // the pool's pieces: its own errors
+
         if (!rc && !chunked) {
             while (fv.done < count && !rc) {
                 rc = reap(c, true);
@@ -2645,6 +2688,51 @@ int64_t vx_verify_files_multi(vx_ctx* const* ctxs, size_t nctx, const char* cons
         const size_t count = base + (k >= extra_from ? 1 : 0);
         rcs[k] = vx_verify_files_range(ctxs[k], paths, file_lengths, nfiles, piece_length, expected, n_pieces,
                                        first, count, matched_out + first, per_ctx);
+        if (rcs[k] < 0) errs[k] = g_err;  // g_err is thread-local
+    };
+    std::vector<std::thread> th;
+    th.reserve(nctx);
+    size_t started = 1;
+    try {
+        for (; started < nctx; ++started) th.emplace_back(run, started);
+    } catch (...) {  // could not start a thread: run the rest on this one
+    }
+    run(0);
+    for (size_t k = started; k < nctx; ++k) run(k);
+    for (auto& t : th) t.join();
+    int64_t nbad = 0;
+    for (size_t k = 0; k < nctx; ++k) {
+        if (rcs[k] < 0) {
+            g_err = "context " + std::to_string(k) + ": " + errs[k];
+            return rcs[k];
+        }
+        nbad += rcs[k];
+    }
+    return nbad;
+}
+
+// The split over several GPUs of one process: one host thread per context,
+// each running vx_verify_files_split on the same claim word, which is
+// declared for nctx engines so each sizes its groups as one of nctx equal
+// takers beside the pool.  io_threads is the total reader count, divided.
+int64_t vx_verify_files_split_multi(vx_ctx* const* ctxs, size_t nctx, const char* const* paths,
+                                    const uint64_t* file_lengths, size_t nfiles, uint32_t piece_length,
+                                    const uint8_t* expected, size_t n_pieces, vx_split* s, uint8_t* matched_out,
+                                    uint32_t io_threads) {
+    if (!ctxs || nctx == 0 || nctx > 1024 || !s) return fail(VX_EINVAL, "vx_verify_files_split_multi: bad argument");
+    for (size_t k = 0; k < nctx; ++k) {
+        if (!ctxs[k]) return fail(VX_EINVAL, "vx_verify_files_split_multi: NULL context");
+        for (size_t j = 0; j < k; ++j)
+            if (ctxs[j] == ctxs[k]) return fail(VX_EINVAL, "vx_verify_files_split_multi: a context appears twice");
+    }
+    s->engines = (uint32_t)nctx;
+    const uint32_t total_io = io_threads ? io_threads : std::max(1u, std::min(16u, usable_cpus()));
+    const uint32_t per_ctx = std::max<uint32_t>(1, total_io / (uint32_t)nctx);
+    std::vector<int64_t> rcs(nctx, 0);
+    std::vector<std::string> errs(nctx);
+    auto run = [&](size_t k) {
+        rcs[k] = vx_verify_files_split(ctxs[k], paths, file_lengths, nfiles, piece_length, expected, n_pieces, s,
+                                       matched_out, per_ctx);
         if (rcs[k] < 0) errs[k] = g_err;  // g_err is thread-local
     };
     std::vector<std::thread> th;

@@ -412,6 +412,27 @@ def verify_files_multi(pools: Sequence["HashPool"], paths: Sequence[str], file_l
     return [bool(b) for b in out.raw[:n]], int(bad)
 
 
+def verify_files_split_multi(pools: Sequence["HashPool"], paths: Sequence[str], file_lengths: Sequence[int],
+                             piece_length: int, expected: bytes, split: "Split", io_threads: int = 0) -> int:
+    """The split over several GPUs (vx_verify_files_split_multi): every pool
+    is one engine claiming from `split` on its own host thread, beside the
+    caller's pool on split.claim().  Verdicts land in split.matched; returns
+    the engines' pieces with I/O errors.  Blocks; run the pool on other
+    threads."""
+    if not pools:
+        raise ValueError("need at least one pool")
+    L = pools[0].lib
+    if any(p.lib is not L for p in pools):
+        raise ValueError("verify_files_split_multi: every pool must come from the same library (hooks)")
+    ctxs = (ctypes.c_void_p * len(pools))(*[p._h.value for p in pools])
+    arr = (ctypes.c_char_p * max(1, len(paths)))(*[os.fsencode(p) for p in paths])
+    lens = (ctypes.c_uint64 * max(1, len(file_lengths)))(*file_lengths)
+    exp = ctypes.create_string_buffer(bytes(expected), max(1, len(expected)))
+    rc = L.vx_verify_files_split_multi(ctxs, len(pools), arr, lens, len(paths), piece_length, exp,
+                                       len(expected) // 20, ctypes.byref(split.s), split.matched, io_threads)
+    return int(check(rc, "vx_verify_files_split_multi", L))
+
+
 def _ptr_arrays(pieces: Sequence):
     n = len(pieces)
     keep = []
