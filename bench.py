@@ -951,7 +951,7 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
     cpu = {"warm": [], "cold": []}
     cpu_ok = True
     pool = None
-    split = None
+    split = balanced = None
     try:
         try:
             pool = HashPool(pl, device=local, slots=4, slot_bytes=512 << 20, batch_pieces=4096)
@@ -1007,6 +1007,7 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
                         cpu_ok = False
                 dist.barrier()
         split = multi_split(rank, world, pool, path, total, n, exp, io_threads, ncpu, cpu, agree, reps)
+        balanced = multi_balanced(rank, world, pool, path, total, n, exp, io_threads, ncpu, cpu, agree, reps)
     finally:
         if pool is not None:
             pool.close()
@@ -1044,6 +1045,9 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
                       "pool_only": out["warm"]["cpu_pool"]["value"] if out["warm"]["cpu_pool"] else None})
         split["beats_both"] = split["value"] > max(v for v in (split["gpu_only"], split["pool_only"]) if v)
         out["split"] = split
+    if balanced is not None:
+        balanced["vs_planned"] = round(balanced["value"] / split["value"], 4) if split else None
+        out["split_balanced"] = balanced
     out.update({"ranks": world, "same_device": same_device, "io_threads_per_rank": io_threads,
                 "pieces": n, "bytes": total, "write_s": round(spec["write_s"], 2), "cpu_pool_verdicts_ok": cpu_ok,
                 "file": {"dir": spec["dir"], "fs": fs_type(spec["dir"])},
@@ -1052,6 +1056,106 @@ def reverify_multi_leg(rank: int, world: int, local: int, dev, backend: str, sam
                           f"warm median of {reps}, cold (evicted) median of {cold_reps}; the slowest rank's time; "
                           f"CPU pool restatement with all {ncpu} node CPUs beside it"})
     return out
+
+
+def multi_balanced(rank, world, pool, path, total, n, exp, io_threads, ncpu, cpu, agree, reps):
+    """The self-balancing split over a node (vx_verify_files_split with one
+    engine per rank): one vx_split and one verdict array in a
+    /dev/shm mapping every rank shares, declared for `world` engines; every
+    rank's engine claims groups from the top on its own GPU while rank 0's CPU
+    pool restatement claims pieces from the head.  A call's time is the
+    slowest side's; rank 0 checks every verdict in the shared array.  Warm
+    only.  Returns the record on rank 0 (None elsewhere)."""
+    import mmap
+    import threading
+
+    import torch.distributed as dist
+
+    import oracle
+    from vortex_amd import _lib
+    from vortex_amd.hash_pool import Split
+
+    pl = 2097152
+    size = ctypes.sizeof(_lib.vx_split) + n
+    name = [None]
+    if rank == 0:
+        name = [f"/dev/shm/vx_bench_split_{os.getpid()}_{time.time_ns()}"]
+        try:
+            with open(name[0], "wb") as f:
+                f.truncate(size)
+        except OSError as e:
+            name = [f"error: {e}"]
+    dist.broadcast_object_list(name, src=0)
+    if name[0].startswith("error"):
+        raise RuntimeError(f"multi-GPU balanced split: no shared mapping ({name[0]})")
+    fd = os.open(name[0], os.O_RDWR)
+    mm = mmap.mmap(fd, size)
+    os.close(fd)
+    pool_threads = max(1, ncpu * 3 // 4)
+    cw = sorted(cpu["warm"])[len(cpu["warm"]) // 2] if cpu["warm"] else None
+    rate = total / cw / ncpu if cw else 0.0
+    times, ok_all, bounds = [], True, []
+    sp = None
+    try:
+        for _ in range(reps):
+            if rank == 0:
+                mm[ctypes.sizeof(_lib.vx_split):] = bytes(n)
+                sp = Split.attach(mm, 0, n, True, pool_threads, rate, engines=world)
+            dist.barrier()
+            if rank != 0:
+                sp = Split.attach(mm, 0, n, False)
+            res, ok = {}, True
+
+            def pool_side():
+                try:
+                    t0 = time.perf_counter()
+                    res["taken"] = oracle.pool_verify_files_claim([path], [total], pl, exp, pool_threads, sp.claim_fn,
+                                                                  sp.done_fn, sp.arg, 0, sp.matched)
+                    res["cpu_s"] = time.perf_counter() - t0
+                except Exception as e:  # noqa: BLE001  (a failed pool is a wrong-verdict run, below)
+                    log(f"balanced split: the CPU pool failed: {type(e).__name__}: {e}")
+
+            th = threading.Thread(target=pool_side) if rank == 0 else None
+            t0 = time.perf_counter()
+            if th:
+                th.start()
+            try:
+                bad = pool.verify_files_split([path], [total], pl, exp, sp, io_threads=io_threads)
+            except Exception as e:  # noqa: BLE001
+                log(f"rank {rank}: balanced split call failed: {type(e).__name__}: {e}")
+                ok, bad = False, 0
+            gpu_s = time.perf_counter() - t0
+            if th:
+                th.join()
+            el = time.perf_counter() - t0
+            if not agree(ok and bad == 0):
+                raise RuntimeError("multi-GPU balanced split: a rank's vx_verify_files_split call failed")
+            dist.barrier()  # every engine has written its verdicts
+            allt = [None] * world
+            dist.all_gather_object(allt, {"s": el, "gpu_s": gpu_s})
+            if rank == 0:
+                ok_all = ok_all and bytes(sp.matched)[:n] == b"\x01" * n
+                bounds.append(sp.boundary)
+                times.append({"s": max(t["s"] for t in allt), "gpu_s": max(t["gpu_s"] for t in allt),
+                              "cpu_s": res.get("cpu_s", 0.0)})
+            sp = None
+            dist.barrier()  # rank 0 re-inits the word only after every rank let go of it
+    finally:
+        sp = None
+        mm.close()
+        if rank == 0:
+            os.unlink(name[0])
+    if rank != 0:
+        return None
+    if not ok_all:
+        raise RuntimeError("multi-GPU balanced split: verdicts differ from the expected table")
+    med = sorted(times, key=lambda t: t["s"])[len(times) // 2]
+    return {"value": round(total / med["s"] / GiB, 2), "unit": "GiB/s", "s": med["s"],
+            "gpu_s": round(med["gpu_s"], 4), "cpu_s": round(med["cpu_s"], 4),
+            "s_runs": [round(t["s"], 4) for t in times], "gpu_first_runs": bounds, "pool_threads": pool_threads,
+            "sample": f"warm; one vx_split and verdict array shared through /dev/shm by the {world} ranks' engines "
+                      f"(engines = {world}) and rank 0's CPU pool restatement; no plan; the slowest side's time, "
+                      f"median of {reps}; every verdict checked"}
 
 
 def multi_split(rank, world, pool, path, total, n, exp, io_threads, ncpu, cpu, agree, reps):

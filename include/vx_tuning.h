@@ -68,8 +68,9 @@ int vx_tuning_plan_ragged(uint32_t n, uint32_t max_len, uint64_t total_len);
 size_t vx_tuning_chunk_schedule(uint64_t L, uint64_t C, int head, int tail, uint64_t* out, size_t max);
 /* The engine's side of the split's claim word (vx_verify_files_split):
  * take up to k pieces from the top of the unclaimed range; returns the new
- * stop, so the engine's pieces are [returned, previous stop) (host-only). */
-uint64_t vx_tuning_split_take_tail(struct vx_split* s, uint64_t k);
+ * stop and (was, may be NULL) the stop before, so the pieces taken are
+ * [returned, *was) (host-only). */
+uint64_t vx_tuning_split_take_tail(struct vx_split* s, uint64_t k, uint64_t* was);
 /* The last vx_verify_files_split call's decisions, one row of 12 doubles per
  * round it formed: ms since the call's start, the pool's rate (pieces/s), the
  * engine's intake rate (B/s), its chain per 64-byte block (ns), the predicted

@@ -37,6 +37,24 @@ class CpuPool:
         count = n - first if count is None else count
         return list(allv[first:first + count]), 0
 
+    def verify_files_split(self, paths, lens, pl, exp, split, io_threads=0):
+        """The engine's side of a split, on the CPU: groups of 3 pieces from
+        the top of the shared claim word (the test build's take-tail hook),
+        each verified with the oracle and written into the shared verdicts."""
+        import ctypes
+
+        from vortex_amd import _lib
+
+        allv = oracle.pool_verify_files(paths, lens, pl, exp, threads=2)
+        tuning = _lib.tuning()
+        while True:
+            was = ctypes.c_uint64()
+            lo = tuning.vx_tuning_split_take_tail(ctypes.byref(split.s), 3, ctypes.byref(was))
+            if lo >= was.value:
+                return 0
+            for i in range(lo, was.value):
+                split.matched[i - split.first] = b"\x01" if allv[i] else b"\x00"
+
     def last_verify(self):
         return {"read_GiBps": 1.0, "copy_busy_frac": 0.5, "direct_bytes": 0}
 

@@ -295,6 +295,7 @@ def test_reverify_multi_leg_rehearsal(built, gpu, tmp_path):
         assert all(len(t) == 2 for t in rm[leg]["rank_traces"])
     _check_plan(rm)
     _check_split(rm)
+    _check_balanced(rm)
 
 
 def _check_split(rm):
@@ -303,6 +304,13 @@ def _check_split(rm):
     sp = rm["split"]
     assert sp["gpu_first"] + sp["gpu_count"] == rm["pieces"] and sp["value"] > 0 and len(sp["s_runs"]) >= 1
     assert sp["gpu_first"] == sp["plan"]["gpu_first"] and isinstance(sp["beats_both"], bool)
+
+
+def _check_balanced(rm):
+    """The node-level balanced split (bench.multi_balanced): one claim word in
+    /dev/shm for every rank's engine and rank 0's pool, every verdict checked."""
+    b = rm["split_balanced"]
+    assert b["value"] > 0 and len(b["s_runs"]) >= 1 and all(0 <= g <= rm["pieces"] for g in b["gpu_first_runs"])
 
 
 def _check_plan(rm):
@@ -339,6 +347,7 @@ def test_reverify_multi_leg_collective_logic_cpu(tmp_path, mode):
             assert rm[leg]["value"] > 0 and all(len(t) == 2 for t in rm[leg]["rank_traces"])
         _check_plan(rm)
         _check_split(rm)
+        _check_balanced(rm)
     else:
         assert "vx_verify_files_range call failed" in d["error"]
     assert not [p for p in os.listdir(tmp_path) if p.startswith("vx_bench_multi_linuxmint")]

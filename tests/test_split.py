@@ -113,7 +113,9 @@ def test_claims_from_both_ends_race(tmp_path, seed):
     def engine():
         stop = n
         while True:
-            new = tuning.vx_tuning_split_take_tail(ctypes.byref(sp.s), rng.randint(1, 9))
+            was = ctypes.c_uint64()
+            new = tuning.vx_tuning_split_take_tail(ctypes.byref(sp.s), rng.randint(1, 9), ctypes.byref(was))
+            assert was.value == stop  # the only engine: the stop is where it left it
             if new == stop:
                 break
             groups.append((new, stop))

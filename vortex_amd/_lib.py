@@ -197,7 +197,7 @@ def _declare(L: ctypes.CDLL, tuning: bool = False) -> None:
             "vx_tuning_wall_clock_khz": ([c.c_int], c.c_int),
             "vx_tuning_device_identity": ([c.c_int, c.c_char_p, c.c_size_t, c.c_char_p], c.c_int),
             "vx_tuning_plan_ragged": ([c.c_uint32, c.c_uint32, c.c_uint64], c.c_int),
-            "vx_tuning_split_take_tail": ([c.POINTER(vx_split), c.c_uint64], c.c_uint64),
+            "vx_tuning_split_take_tail": ([c.POINTER(vx_split), c.c_uint64, c.POINTER(c.c_uint64)], c.c_uint64),
             "vx_tuning_last_split": ([vp, c.POINTER(c.c_double), c.c_size_t], c.c_size_t),
             "vx_tuning_chunk_schedule": ([c.c_uint64, c.c_uint64, c.c_int, c.c_int, c.POINTER(c.c_uint64),
                                           c.c_size_t], c.c_size_t),

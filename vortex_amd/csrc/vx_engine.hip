@@ -3016,7 +3016,9 @@ void vx_tuning_stage_huge(vx_ctx* c, int on) {
         if (s.state == Slot::FREE) free_stage(s);
 }
 #endif
-uint64_t vx_tuning_split_take_tail(vx_split* s, uint64_t k) { return s ? split_take_tail(s, k) : 0; }
+uint64_t vx_tuning_split_take_tail(vx_split* s, uint64_t k, uint64_t* was) {
+    return s ? split_take_tail(s, k, UINT64_MAX, was) : 0;
+}
 size_t vx_tuning_last_split(const vx_ctx* c, double* out, size_t max) {
     if (!c) return 0;
     const size_t k = std::min(max, c->last_split.size());

@@ -370,6 +370,28 @@ class Split:
         self.claim_fn = ctypes.cast(self.lib.vx_split_claim, ctypes.c_void_p).value
         self.done_fn = ctypes.cast(self.lib.vx_split_done, ctypes.c_void_p).value
 
+    @classmethod
+    def attach(cls, buf, first: int, end: int, init: bool, cpu_threads: int = 0, cpu_thread_rate: float = 0.0,
+               engines: int = 1) -> "Split":
+        """A split living in a shared buffer (e.g. a MAP_SHARED mmap of a
+        /dev/shm file, one per node): the vx_split at offset 0, the end - first
+        verdict bytes after it, so engines in several processes (one per GPU)
+        and the pool claim from one word and write one verdict array.  One
+        process inits (init=True) before the others attach."""
+        self = cls.__new__(cls)
+        self.lib = lib()
+        self.s = _lib.vx_split.from_buffer(buf, 0)
+        if init:
+            check(self.lib.vx_split_init(ctypes.byref(self.s), first, end, cpu_threads, cpu_thread_rate),
+                  "vx_split_init", self.lib)
+            self.s.engines = engines
+        self.first, self.end = first, end
+        self.matched = (ctypes.c_char * max(1, end - first)).from_buffer(buf, ctypes.sizeof(_lib.vx_split))
+        self.arg = ctypes.addressof(self.s)
+        self.claim_fn = ctypes.cast(self.lib.vx_split_claim, ctypes.c_void_p).value
+        self.done_fn = ctypes.cast(self.lib.vx_split_done, ctypes.c_void_p).value
+        return self
+
     def claim(self) -> int:
         """The next piece for the pool, or -1 when none is left."""
         return int(self.lib.vx_split_claim(ctypes.byref(self.s)))
@@ -387,7 +409,7 @@ class Split:
         return int(self.s.pool_done)
 
     def verdicts(self) -> list[bool]:
-        return [bool(b) for b in self.matched.raw[:self.end - self.first]]
+        return [bool(b) for b in bytes(self.matched)[:self.end - self.first]]
 
 
 def verify_files_multi(pools: Sequence["HashPool"], paths: Sequence[str], file_lengths: Sequence[int],
