@@ -7,8 +7,9 @@
   itself, as vortex's pool would; every piece must come back exactly once
   with hashlib's verdict, and the engine's counters must agree.
 * The re-verify of random multi-file torrents (damaged, truncated and
-  missing files) through the chunk rounds' copy stream, whole and split with
-  the CPU pool restatement at random points (bench.split_call): every verdict
+  missing files) through the chunk rounds' copy stream, whole, split with the
+  CPU pool restatement at random points (bench.split_call) and balanced at run
+  time (bench.balanced_call, vx_verify_files_split): every verdict
   equals oracle.pool_verify_files (file_store.rs:228-303 restated), and every
   chunk round's timeline is ordered.
 """
@@ -148,5 +149,9 @@ def test_soak_reverify_and_split(built, gpu, tmp_path):
             first = rng.randint(0, n)
             r = bench.split_call(pool, paths, sizes, n, pl, exp, first, rng.choice([2, 4]), rng.choice([2, 4]))
             assert r["matched"] == want, (sizes, pl, first)
+            # the self-balancing split, pool of any size and any claimed rate
+            b = bench.balanced_call(pool, paths, sizes, n, pl, exp, rng.choice([1, 2, 4]), rng.choice([1, 2, 4, 8]),
+                                    rng.choice([0.0, 3e8, 2e9, 2e10]))
+            assert b["matched"] == want and 0 <= b["boundary"] <= n, (sizes, pl, b["boundary"])
         torrents += 1
     assert torrents >= 5
