@@ -2080,7 +2080,10 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
                         rc = fail(VX_EINVAL, "vx_verify_files_split: another engine claims from this split");
                         return -1;
                     }
-                    if (lo < old) mine.emplace_back(lo, old);
+                    if (lo < old && !mine.empty() && mine.back().first == old)
+                        mine.back().first = lo;  // right below the last group: one range (one D2H)
+                    else if (lo < old)
+                        mine.emplace_back(lo, old);
                     for (uint64_t i = lo; i < old; ++i) lanes.push_back(Lane{i, 0, !formed_any});
                     *lowest = std::min(*lowest, lo);
                 }
