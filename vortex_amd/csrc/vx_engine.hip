@@ -1840,6 +1840,13 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
     // end (a copy that waited for its reads counts the wait).
     double in_bytes = 0, in_ms = 0, in_n = 0;
     float first_cs = -1;
+    // every measured copy: (end ms, bytes, longest chunk), for the steady-state
+    // intake the next call starts from
+    struct CopyEnd {
+        double end_ms;
+        uint64_t bytes, max_chunk;
+    };
+    std::vector<CopyEnd> copy_ends;
     std::vector<double> block_ns;         // measured chain per 64-byte block, one per round
     std::vector<uint64_t> timed_bytes;
     std::vector<vx_verify_round> tl;
@@ -1882,6 +1889,7 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
                     in_bytes += (double)r.bytes;
                     in_ms = (double)ce - (double)first_cs;
                     in_n += 1;
+                    copy_ends.push_back(CopyEnd{(double)ce, r.bytes, r.max_chunk});
                 }
             }
             ++copied_upto;
@@ -2220,7 +2228,19 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
         // call's whole-call figures, averaged with the earlier calls' at 1/2
         measure();
         auto mean = [](double& m, double v) { m = m > 0 ? 0.5 * (m + v) : v; };
-        if (in_n >= 2 && in_ms > 0) mean(c->split_rin, in_bytes / (in_ms * 1e-3));
+        // the steady-state intake: the full-chunk rounds' bytes over the time
+        // from the copy before the first of them to the last one's end (the
+        // ramps' short rounds and the chain-bound tail would understate it,
+        // and the next call would claim too little)
+        {
+            size_t a = copy_ends.size(), b = 0;
+            for (size_t k = 0; k < copy_ends.size(); ++k)
+                if (copy_ends[k].max_chunk >= C) a = std::min(a, k), b = k;
+            double bytes = 0;
+            for (size_t k = a + 1; k <= b && a < copy_ends.size(); ++k) bytes += (double)copy_ends[k].bytes;
+            const double ms = a < b ? copy_ends[b].end_ms - copy_ends[a].end_ms : 0.0;
+            if (ms > 0 && bytes > 0) mean(c->split_rin, bytes / (ms * 1e-3));
+        }
         if (!block_ns.empty()) {
             std::nth_element(block_ns.begin(), block_ns.begin() + block_ns.size() / 2, block_ns.end());
             mean(c->split_bns, block_ns[block_ns.size() / 2]);
