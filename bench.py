@@ -772,11 +772,16 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
                 bal.append(balanced_call(pool, [path], [total], n, pl, exp, io_t, pool_t, rate))
             assert all(b["ok"] for b in bal), "balanced split: a verdict differs from the expected table"
             bm = sorted(bal, key=lambda b: b["s"])[len(bal) // 2]
+            # each side's own rate in the median call: the engine's pieces
+            # [boundary, n) over its time, the pool's [0, boundary) over its
+            eng_bytes = total - bm["boundary"] * pl
             split["balanced"] = {"io_threads": io_t, "cpu_threads": pool_t, "value": round(total / bm["s"] / GiB, 2),
                                  "s_runs": [round(b["s"], 4) for b in bal],
                                  "gpu_first_runs": [b["boundary"] for b in bal],
                                  "gpu_s": round(bm["gpu_s"], 4), "cpu_s": round(bm["cpu_s"], 4),
-                                 "gpu_first": bm["boundary"]}
+                                 "gpu_first": bm["boundary"],
+                                 "engine_GiBps": round(eng_bytes / bm["gpu_s"] / GiB, 2) if bm["gpu_s"] else None,
+                                 "pool_GiBps": round((total - eng_bytes) / bm["cpu_s"] / GiB, 2) if bm["cpu_s"] else None}
             for (first, io_c, pool_c), calls in by_cfg.items():
                 assert all(c["ok"] for c in calls), "split re-verify: a verdict differs from the expected table"
                 med = sorted(calls, key=lambda c: c["s"])[len(calls) // 2]
