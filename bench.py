@@ -851,6 +851,8 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
                   "planned_value": pv, "planned_vs_best_fixed": round(pv / best["value"], 4),
                   "best_value": best["value"], "best_gpu_first": best["gpu_first"],
                   "best_io_threads": best["io_threads"], "balanced_gpu_first": split["balanced"]["gpu_first"],
+                  "balanced_engine_GiBps": split["balanced"]["engine_GiBps"],
+                  "balanced_pool_GiBps": split["balanced"]["pool_GiBps"],
                   "gpu_only": split["gpu_alone"]["value"], "pool_only": split["pool_alone"]["value"],
                   # against the better of each side's two figures: in the alternation and in the legs above
                   "beats_both": bv > either, "planned_beats_both": pv > either,
