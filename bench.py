@@ -1095,9 +1095,21 @@ def multi_balanced(rank, world, pool, path, total, n, exp, io_threads, ncpu, cpu
     dist.broadcast_object_list(name, src=0)
     if name[0].startswith("error"):
         raise RuntimeError(f"multi-GPU balanced split: no shared mapping ({name[0]})")
-    fd = os.open(name[0], os.O_RDWR)
-    mm = mmap.mmap(fd, size)
-    os.close(fd)
+    mm = None
+    try:
+        fd = os.open(name[0], os.O_RDWR)
+        try:
+            mm = mmap.mmap(fd, size)
+        finally:
+            os.close(fd)
+    except OSError as e:
+        log(f"rank {rank}: cannot map the shared split: {e}")
+    if not agree(mm is not None):  # every rank maps it, or every rank stops here
+        if mm is not None:
+            mm.close()
+        if rank == 0:
+            os.unlink(name[0])
+        raise RuntimeError("multi-GPU balanced split: a rank could not map the shared split")
     pool_threads = max(1, ncpu * 3 // 4)
     cw = sorted(cpu["warm"])[len(cpu["warm"]) // 2] if cpu["warm"] else None
     rate = total / cw / ncpu if cw else 0.0
