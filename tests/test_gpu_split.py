@@ -228,3 +228,33 @@ def test_split_multi_engines(built, gpu, tmp_path, nctx, cpu_threads):
     finally:
         for p in pools:
             p.close()
+
+
+def test_split_stats_count_the_engines_pieces_only(built, gpu, tmp_path):
+    """vx_get_stats after a split: the engine counts exactly its own pieces
+    [boundary, end) — completed, mismatched (damaged, not I/O errors) and I/O
+    errors (a truncated tail file) — and none of the pool's."""
+    from vortex_amd.hash_pool import HashPool
+
+    pl, n_a, n_b = 1 << 20, 120, 40
+    sizes = [n_a * pl, n_b * pl - 777]
+    paths, sizes, exp = _files(tmp_path, pl, sizes, 61)
+    n = len(exp) // 20
+    with open(paths[1], "r+b") as f:  # damage a piece near the top (the engine's side)
+        f.seek(30 * pl + 11)
+        b = f.read(1)
+        f.seek(30 * pl + 11)
+        f.write(bytes([b[0] ^ 0x80]))
+    os.truncate(paths[1], 37 * pl)  # pieces n_a+37 .. n-1 short or missing: I/O errors
+    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
+    with HashPool(pl, slots=3, slot_bytes=64 << 20) as pool:
+        pool.reset_stats()
+        sp, taken, bad = _run_split(pool, paths, sizes, pl, exp, 0, n, 2, io_threads=4)
+        b = sp.boundary
+        assert sp.verdicts() == want and taken == b
+        assert b <= n_a + 30, b  # the engine took the top (a 2-thread pool cannot reach it first)
+        st = pool.stats()
+        io_err = [i for i in range(b, n) if i >= n_a + 37]
+        assert bad == len(io_err) == st["io_errors"]
+        assert st["pieces_completed"] == n - b
+        assert st["pieces_mismatched"] == sum(1 for i in range(b, n) if not want[i]) - len(io_err)
