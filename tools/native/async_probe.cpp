@@ -11,7 +11,7 @@
 // line: GiB/s of piece bytes submitted → verdict polled.
 //
 // usage: async_probe <piece_len> [nbuf=1024] [total_GiB=8] [flush_every=64] [registered=1] [slot_MiB=default (0)] [slots=4]
-//                    [overflow_threads=0]
+//                    [overflow_threads=0] [cap=model|measured]
 //   registered: 0 = plain memory (staged), 1 = one registered mmap holding all
 //   buffers, 2 = one mmap per buffer, each registered (vortex's BufferPool,
 //   buf_pool.rs:92-98)
@@ -24,6 +24,9 @@
 //   batch latency of work (vx_plan_verify's piece_latency_s over
 //   cpu_piece_latency_s, times the pool's threads); otherwise it polls and
 //   offers the piece to the engine again (both sides full).
+//   [cap=model|measured]: "measured" sets that bound from this run instead:
+//   the engine's mean batch latency over the warm-up (vx_get_stats) over one
+//   piece's SHA-1 time on this host, times the pool's threads.
 #include <sys/mman.h>
 
 #include <algorithm>
@@ -118,6 +121,7 @@ int main(int argc, char** argv) {
     }
     if (argc > 7) cfg.slots = (uint32_t)std::atoi(argv[7]);  // batch slots (default 4)
     const int overflow_threads = argc > 8 ? std::atoi(argv[8]) : 0;
+    const bool cap_measured = argc > 9 && std::strcmp(argv[9], "measured") == 0;
     cfg.refuse_when_full = overflow_threads > 0 ? 1 : 0;
     vx_ctx* ctx = nullptr;
     if (int rc = vx_create(&cfg, &ctx)) {
@@ -176,6 +180,7 @@ int main(int argc, char** argv) {
     };
     // warm-up: four passes over the pool with the timed flush cadence, so
     // every slot has run (and allocated its pinned stage, if it needs one)
+    vx_reset_stats(ctx);  // the warm-up's batch latency (cap=measured)
     uint64_t sent = 0;
     for (int pass = 0; pass < 4; ++pass) {
         std::shuffle(order.begin(), order.end(), rng);
@@ -196,12 +201,26 @@ int main(int argc, char** argv) {
     sent = 0;
     Overflow ov;
     size_t backlog_cap = 0;
+    double gpu_latency_s = 0, cpu_piece_s = 0;
     if (overflow_threads > 0) {
+        if (cap_measured) {
+            vx_stats ws{};
+            vx_get_stats(ctx, &ws);
+            gpu_latency_s = ws.batch_latency_count ? ws.batch_latency_sum_us * 1e-6 / ws.batch_latency_count : 0.0;
+            uint8_t d[20];
+            const int k = 8;
+            const double c0 = now_s();
+            for (int i = 0; i < k; ++i) vxo_sha1_backend(ptrs[i % nbuf], plen, d, 0);
+            cpu_piece_s = (now_s() - c0) / k;
+        } else {
+            vx_plan pl{};
+            vx_plan_verify(1, plen, plen, (uint32_t)overflow_threads, 0.0, &pl);
+            gpu_latency_s = pl.piece_latency_s;
+            cpu_piece_s = pl.cpu_piece_latency_s;
+        }
         ov.start(overflow_threads, ptrs, plen, digests);
-        vx_plan pl{};
-        vx_plan_verify(1, plen, plen, (uint32_t)overflow_threads, 0.0, &pl);
         backlog_cap = (size_t)overflow_threads *
-                      (size_t)std::max(1.0, std::round(pl.piece_latency_s / std::max(1e-9, pl.cpu_piece_latency_s)));
+                      (size_t)std::max(1.0, std::round(gpu_latency_s / std::max(1e-9, cpu_piece_s)));
     }
     uint64_t refused = 0, to_cpu = 0;
     vx_reset_stats(ctx);  // the engine's own view of the timed region (vx_get_stats)
@@ -252,13 +271,15 @@ int main(int argc, char** argv) {
     vx_destroy(ctx);
     for (uint8_t* m : maps) munmap(m, map_bytes);
     std::printf("{\"piece_len\": %u, \"pieces\": %llu, \"registered\": %d, \"flush_every\": %u, \"GiBps\": %.3f, "
-                "\"overflow_threads\": %d, \"backlog_cap\": %zu, \"refused\": %llu, \"cpu_pieces\": %llu, "
+                "\"overflow_threads\": %d, \"backlog_cap\": %zu, \"cap\": \"%s\", \"cap_gpu_latency_ms\": %.3f, "
+                "\"cap_cpu_piece_ms\": %.4f, \"refused\": %llu, \"cpu_pieces\": %llu, "
                 "\"mismatched\": %llu, \"polled\": %llu, \"engine\": {\"batches\": %llu, \"pieces_completed\": %llu, "
                 "\"gather_tiles\": %llu, \"staged_bytes\": %llu, \"submit_stall_ms\": %.3f, "
                 "\"batch_latency_mean_ms\": %.3f, \"batch_latency_max_ms\": %.3f, "
                 "\"batch_latency_median_bucket_ms\": [%.3f, %.3f]}}\n",
                 plen, (unsigned long long)total, registered, flush_every,
-                (double)total * plen / el / (1 << 30), overflow_threads, backlog_cap, (unsigned long long)refused,
+                (double)total * plen / el / (1 << 30), overflow_threads, backlog_cap,
+                cap_measured ? "measured" : "model", gpu_latency_s * 1e3, cpu_piece_s * 1e3, (unsigned long long)refused,
                 (unsigned long long)ov.done.load(), (unsigned long long)bad, (unsigned long long)polled,
                 (unsigned long long)st.batches, (unsigned long long)st.pieces_completed,
                 (unsigned long long)st.gather_tiles, (unsigned long long)st.staged_bytes, st.submit_stall_ns * 1e-6,
