@@ -356,19 +356,12 @@ class Split:
     finished one with done(); the engine (HashPool.verify_files_split) takes
     groups from the top, sized from both sides' rates measured as it goes.
     `matched` holds every verdict once both sides have returned: entries
-    [0, boundary - first) are the pool's to write, the rest the engine's.
+    [0, boundary - first) are the pool's to write, the rest the engines'.
     claim_fn / done_fn / arg are the C addresses a native pool calls."""
 
     def __init__(self, first: int, end: int, cpu_threads: int = 0, cpu_thread_rate: float = 0.0):
-        self.lib = lib()
-        self.s = _lib.vx_split()
-        check(self.lib.vx_split_init(ctypes.byref(self.s), first, end, cpu_threads, cpu_thread_rate),
-              "vx_split_init", self.lib)
-        self.first, self.end = first, end
-        self.matched = ctypes.create_string_buffer(max(1, end - first))
-        self.arg = ctypes.addressof(self.s)
-        self.claim_fn = ctypes.cast(self.lib.vx_split_claim, ctypes.c_void_p).value
-        self.done_fn = ctypes.cast(self.lib.vx_split_done, ctypes.c_void_p).value
+        self._bind(_lib.vx_split(), ctypes.create_string_buffer(max(1, end - first)), first, end)
+        self._init(cpu_threads, cpu_thread_rate, 1)
 
     @classmethod
     def attach(cls, buf, first: int, end: int, init: bool, cpu_threads: int = 0, cpu_thread_rate: float = 0.0,
@@ -379,18 +372,24 @@ class Split:
         and the pool claim from one word and write one verdict array.  One
         process inits (init=True) before the others attach."""
         self = cls.__new__(cls)
-        self.lib = lib()
-        self.s = _lib.vx_split.from_buffer(buf, 0)
+        self._bind(_lib.vx_split.from_buffer(buf, 0),
+                   (ctypes.c_char * max(1, end - first)).from_buffer(buf, ctypes.sizeof(_lib.vx_split)), first, end)
         if init:
-            check(self.lib.vx_split_init(ctypes.byref(self.s), first, end, cpu_threads, cpu_thread_rate),
-                  "vx_split_init", self.lib)
-            self.s.engines = engines
+            self._init(cpu_threads, cpu_thread_rate, engines)
+        return self
+
+    def _bind(self, s, matched, first: int, end: int) -> None:
+        self.lib = lib()
+        self.s, self.matched = s, matched
         self.first, self.end = first, end
-        self.matched = (ctypes.c_char * max(1, end - first)).from_buffer(buf, ctypes.sizeof(_lib.vx_split))
         self.arg = ctypes.addressof(self.s)
         self.claim_fn = ctypes.cast(self.lib.vx_split_claim, ctypes.c_void_p).value
         self.done_fn = ctypes.cast(self.lib.vx_split_done, ctypes.c_void_p).value
-        return self
+
+    def _init(self, cpu_threads: int, cpu_thread_rate: float, engines: int) -> None:
+        check(self.lib.vx_split_init(ctypes.byref(self.s), self.first, self.end, cpu_threads, cpu_thread_rate),
+              "vx_split_init", self.lib)
+        self.s.engines = engines
 
     def claim(self) -> int:
         """The next piece for the pool, or -1 when none is left."""
