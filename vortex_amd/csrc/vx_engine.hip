@@ -1763,16 +1763,20 @@ uint64_t split_take_tail(vx_split* s, uint64_t k, uint64_t expect = UINT64_MAX, 
 // the group that joins it (batch_chunked_gather's streaming rounds, here with
 // the group sized at run time).  Before forming a round the engine estimates
 //   T_engine(j) = the rounds its lanes (and j new pieces) still need, each
-//                 max(bytes / min(copy rate, read rate), longest chunk's chain)
-//   T_pool(j)   = (unclaimed - j + the pool's pieces in hand) / pool rate
-// and takes the largest j with T_engine(j) <= T_pool(j).  Every rate is
-// measured in this call: the copy rate and the chain per 64-byte block from
-// the GPU events around each round's copy and kernel, the read rate from the
-// readers' busy time, the pool's rate from vx_split_done.  The first group
-// comes from the cold-start rates (the caller's per-thread rate, the PCIe
-// rate, the kernel's chain per block); no other group is formed until both
-// sides have measured rates.  The engine's pieces are the contiguous tail
-// [*lowest, end) of the range.
+//                 max(bytes / intake, longest chunk's chain), plus the first
+//                 round's read and the last kernel's chain
+//   T_pool(j)   = (unclaimed - engines x j + half the pool's pieces in hand)
+//                 / the pool's pace
+// and takes the largest j with T_engine(j) <= T_pool(j).  The rates are
+// measured in this call — the intake from the GPU copy events (first copy
+// start to last copy end), the chain per 64-byte block from the kernel
+// events, the pool's pace over its last 4 ms of vx_split_done — except for
+// the first group, which starts from earlier split calls on this context (or
+// the caller's per-thread rate, the PCIe rate and kChainBlock).  No later
+// group is formed until both sides have rates, and one only if it rides the
+// active lanes' rounds and shortens the predicted end by a tenth.  Alone on
+// the split (engines 1) the engine's pieces are the contiguous tail
+// [*lowest, end); beside other engines, the groups it took.
 int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n, uint32_t pl, uint64_t total,
                  uint64_t C, uint64_t* lowest) {
     vx_ctx* c = fv.c;
@@ -2224,8 +2228,8 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
         for (const auto& r : rows)
             for (uint64_t i = r.first; i < r.second; ++i)
                 if (fv.bad[i]) fv.matched_out[i] = 0;
-        // the next split call's cold start (this host, this load): each
-        // call's whole-call figures, averaged with the earlier calls' at 1/2
+        // the next split call's cold start (this host, this load): this
+        // call's figures, averaged with the earlier calls' at 1/2
         measure();
         auto mean = [](double& m, double v) { m = m > 0 ? 0.5 * (m + v) : v; };
         // the steady-state intake: the full-chunk rounds' bytes over the time
