@@ -155,3 +155,69 @@ def test_soak_reverify_and_split(built, gpu, tmp_path):
             assert b["matched"] == want and 0 <= b["boundary"] <= n, (sizes, pl, b["boundary"])
         torrents += 1
     assert torrents >= 5
+
+
+def test_soak_split_engines(built, gpu, tmp_path):
+    """The balanced split on random torrents (damaged, truncated and missing
+    files), random ranges, pools of 0-8 threads at any claimed rate, 1-3
+    engines on one split (vx_verify_files_split_multi), random slot sizes and,
+    now and then, an engine round that fails (injected): every verdict of a
+    clean call equals oracle.pool_verify_files; a failed call leaves the
+    context usable and its pieces [boundary, end) to the caller, who verifies
+    them with the oracle.  VX_SOAK_SECONDS (default 10) sets the budget."""
+    import threading
+
+    from vortex_amd._lib import VxError
+    from vortex_amd.hash_pool import HashPool, Split, verify_files_split_multi
+
+    rng = random.Random(77)
+    t_end = time.time() + float(os.environ.get("VX_SOAK_SECONDS", "10"))
+    calls = failed = 0
+    while time.time() < t_end:
+        pl = rng.choice([64 << 10, 256 << 10, 1 << 20, 2 << 20])
+        d = tmp_path / f"s{calls}"
+        d.mkdir()
+        paths, sizes, exp = _torrent(str(d), rng, pl, 1000 + calls)
+        n = len(exp) // 20
+        want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
+        first = rng.randint(0, n // 2)
+        end = rng.randint(first, n)
+        nctx = rng.choice([1, 1, 2, 3])
+        threads = rng.choice([0, 1, 2, 4, 8])
+        inject = rng.random() < 0.2
+        pools = [HashPool(pl, slots=rng.choice([2, 3, 4]), slot_bytes=max(pl, rng.choice([4, 16, 64]) << 20),
+                          hooks=inject) for _ in range(nctx)]
+        try:
+            if inject:
+                pools[rng.randrange(nctx)].lib.vx_tuning_fail_launch_after(
+                    pools[rng.randrange(nctx)]._h, rng.randint(0, 4))
+            sp = Split(first, end, threads, rng.choice([0.0, 3e8, 2e9, 2e10]))
+            out = {}
+
+            def engines():
+                try:
+                    out["bad"] = (verify_files_split_multi(pools, paths, sizes, pl, exp, sp, io_threads=2 * nctx)
+                                  if nctx > 1 else pools[0].verify_files_split(paths, sizes, pl, exp, sp,
+                                                                               io_threads=rng.choice([1, 2, 4])))
+                except VxError as e:
+                    out["err"] = e
+
+            th = threading.Thread(target=engines)
+            th.start()
+            if threads:
+                oracle.pool_verify_files_claim(paths, sizes, pl, exp, threads, sp.claim_fn, sp.done_fn, sp.arg,
+                                               first, sp.matched)
+            th.join()
+            got = sp.verdicts()
+            if "err" in out:  # the caller verifies the engines' side itself
+                failed += 1
+                b = sp.boundary
+                got[b - first:] = want[b:end]
+            assert got == want[first:end], (pl, n, first, end, nctx, threads, sp.boundary)
+            if not threads:
+                assert sp.boundary == first or "err" in out
+        finally:
+            for p in pools:
+                p.close()
+        calls += 1
+    assert calls >= 5
