@@ -218,11 +218,17 @@ int pool_verify_files_impl(const char* const* paths, const uint64_t* lens, size_
     for (size_t f = 0; f < nfiles; ++f) fds[f] = open(paths[f], O_RDONLY | O_CLOEXEC);
     Mpsc ch;
     std::vector<uint8_t> result(n, 0);
+    // backend bit 0x100 (diagnostics only, tools/split_alloc_ab.py): read each
+    // segment into one buffer per thread instead of a fresh zeroed Vec per
+    // segment (file_store.rs:272), to see what the allocation costs the host
+    const bool reuse = (backend & 0x100) != 0;
+    const int sha_backend = backend & 0xff;
     auto job = [&](size_t idx) {
         DownloadedPiece p;
         p.index = idx;
         std::vector<uint8_t> ctx(vxo_sha1_ctx_size());
-        vxo_sha1_init(ctx.data(), backend);
+        vxo_sha1_init(ctx.data(), sha_backend);
+        thread_local std::vector<uint8_t> reused;
         const int64_t piece = (int64_t)idx;
         int64_t total = 0;
         bool ok = true;
@@ -233,14 +239,20 @@ int pool_verify_files_impl(const char* const* paths, const uint64_t* lens, size_
             const int64_t to_read =
                 piece == s.ep ? s.eo - total : std::min<int64_t>((int64_t)piece_length - total, s.len);
             if (to_read <= 0) continue;
-            std::vector<uint8_t> buffer((size_t)to_read);  // vec![0u8; to_read]
+            std::vector<uint8_t> fresh;
+            if (reuse) {
+                if (reused.size() < (size_t)to_read) reused.resize((size_t)to_read);
+            } else {
+                fresh.assign((size_t)to_read, 0);  // vec![0u8; to_read]
+            }
+            uint8_t* buffer = reuse ? reused.data() : fresh.data();
             int64_t got = 0;
             while (got < to_read && ok) {
-                const ssize_t r = fds[f] < 0 ? -1 : pread(fds[f], buffer.data() + got, (size_t)(to_read - got), off + got);
+                const ssize_t r = fds[f] < 0 ? -1 : pread(fds[f], buffer + got, (size_t)(to_read - got), off + got);
                 if (r <= 0) ok = false;
                 else got += r;
             }
-            if (ok) vxo_sha1_update(ctx.data(), buffer.data(), buffer.size());
+            if (ok) vxo_sha1_update(ctx.data(), buffer, (size_t)to_read);
             total += to_read;
         }
         vxo_sha1_final(ctx.data(), p.digest);
