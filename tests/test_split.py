@@ -135,3 +135,74 @@ def test_claims_from_both_ends_race(tmp_path, seed):
     assert tiled == n
     want = oracle.pool_verify_files(paths, lens, pl, exp)
     assert sp.verdicts()[:b - first] == want[first:b]
+
+
+_ATTACH_CHILD = r"""
+import ctypes, mmap, os, sys
+sys.path.insert(0, sys.argv[1])
+import oracle
+from vortex_amd import _lib
+from vortex_amd.hash_pool import Split
+role, shm, n, pl = sys.argv[2], sys.argv[3], int(sys.argv[4]), int(sys.argv[5])
+paths, lens = sys.argv[6].split(','), [int(x) for x in sys.argv[7].split(',')]
+exp = bytes.fromhex(open(sys.argv[8]).read())
+fd = os.open(shm, os.O_RDWR)
+mm = mmap.mmap(fd, ctypes.sizeof(_lib.vx_split) + n)
+os.close(fd)
+sp = Split.attach(mm, 0, n, False)
+if role == "pool":
+    print(oracle.pool_verify_files_claim(paths, lens, pl, exp, 3, sp.claim_fn, sp.done_fn, sp.arg, 0, sp.matched))
+else:  # an engine stand-in: groups from the top, verified with the oracle
+    allv = oracle.pool_verify_files(paths, lens, pl, exp, threads=2)
+    t = _lib.tuning()
+    taken = 0
+    while True:
+        was = ctypes.c_uint64()
+        lo = t.vx_tuning_split_take_tail(ctypes.byref(sp.s), 5, ctypes.byref(was))
+        if lo >= was.value:
+            break
+        for i in range(lo, was.value):
+            sp.matched[i] = b"\x01" if allv[i] else b"\x00"
+        taken += was.value - lo
+    print(taken)
+sp = None
+mm.close()
+"""
+
+
+def test_split_shared_across_processes(tmp_path):
+    """The /dev/shm form of the split (Split.attach; bench.multi_balanced at
+    N > 1): a claim pool in one process and two engine stand-ins in two
+    others claim from one word and write one verdict array; every piece is
+    taken once and every verdict is the plain pool's."""
+    import mmap
+
+    from vortex_amd import _lib
+    from vortex_amd.hash_pool import Split
+
+    pl = 2048
+    paths, exp = _layout(tmp_path, pl, [40 * pl + 3, 7, 55 * pl], seed=21)
+    lens = [os.path.getsize(p) for p in paths]
+    n = len(exp) // 20
+    with open(paths[2], "r+b") as f:
+        f.seek(9 * pl)
+        f.write(b"\xab")
+    want = oracle.pool_verify_files(paths, lens, pl, exp)
+    shm = tmp_path / "split.shm"
+    size = ctypes.sizeof(_lib.vx_split) + n
+    shm.write_bytes(bytes(size))
+    fd = os.open(shm, os.O_RDWR)
+    mm = mmap.mmap(fd, size)
+    os.close(fd)
+    Split.attach(mm, 0, n, True, 3, 0.0, engines=2)
+    (tmp_path / "exp.hex").write_text(exp.hex())
+    args = [ROOT, str(shm), str(n), str(pl), ",".join(paths), ",".join(map(str, lens)), str(tmp_path / "exp.hex")]
+    procs = [subprocess.Popen([os.sys.executable, "-c", _ATTACH_CHILD, args[0], role] + args[1:],
+                              stdout=subprocess.PIPE, text=True) for role in ("engine", "pool", "engine")]
+    taken = [int(p.communicate(timeout=240)[0].split()[-1]) for p in procs]
+    assert all(p.returncode == 0 for p in procs)
+    sp = Split.attach(mm, 0, n, False)
+    assert sum(taken) == n and taken[1] == sp.boundary and sp.pool_done == taken[1]
+    assert sp.verdicts() == want
+    sp = None
+    mm.close()
