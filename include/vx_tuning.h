@@ -57,6 +57,13 @@ void vx_tuning_verify_copy_stream(struct vx_ctx* ctx, int mode);
  * 2 MiB-aligned transparent-huge-page mappings registered with hipHostRegister,
  * 0 with hipHostMalloc.  Idle stages are freed and reallocated on next use. */
 void vx_tuning_stage_huge(struct vx_ctx* ctx, int on);
+/* A/B of the split's rules for pieces of one chunk (vx_verify_files_split,
+ * DESIGN.md §6.6): one_round = 1 (the default) lets their groups keep the
+ * first group's rule until the rates are in and skips the tenth rule, 0 gives
+ * them the multi-round pieces' rules; round_cap > 0 (default 64 MiB) caps
+ * their rounds at that many bytes but no fewer than 1,024 lanes, 0 gives them
+ * the slot's whole stage. */
+void vx_tuning_split_rules(struct vx_ctx* ctx, int one_round, uint64_t round_cap);
 /* The kernel vx_sha1_device_ragged_hint runs for a batch of n pieces whose
  * longest is max_len bytes, total_len bytes in all: 1 = lane, 2 = split,
  * 5 = split with one pair per CU (host-only). */

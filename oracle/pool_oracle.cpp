@@ -216,7 +216,6 @@ int pool_verify_files_impl(const char* const* paths, const uint64_t* lens, size_
     }
     std::vector<int> fds(nfiles);
     for (size_t f = 0; f < nfiles; ++f) fds[f] = open(paths[f], O_RDONLY | O_CLOEXEC);
-    Mpsc ch;
     std::vector<uint8_t> result(n, 0);
     // backend bit 0x100 (diagnostics only, tools/split_alloc_ab.py): read each
     // segment into one buffer per thread instead of a fresh zeroed Vec per
@@ -226,7 +225,8 @@ int pool_verify_files_impl(const char* const* paths, const uint64_t* lens, size_
     auto job = [&](size_t idx) {
         DownloadedPiece p;
         p.index = idx;
-        std::vector<uint8_t> ctx(vxo_sha1_ctx_size());
+        thread_local std::vector<uint8_t> ctx;  // the hasher (sha1::Sha1::new(), on the stack in vortex)
+        ctx.resize(vxo_sha1_ctx_size());
         vxo_sha1_init(ctx.data(), sha_backend);
         thread_local std::vector<uint8_t> reused;
         const int64_t piece = (int64_t)idx;
@@ -263,24 +263,31 @@ int pool_verify_files_impl(const char* const* paths, const uint64_t* lens, size_
             result[idx] = p.hash_matched ? 1 : 0;
         return p;
     };
-    int64_t taken = 0;
-    if (cl) {
-        std::atomic<int64_t> count{0};
-        std::vector<std::thread> ws;
-        for (int t = 0; t < std::max(1, threads); ++t)
-            ws.emplace_back([&] {
-                for (int64_t i; (i = cl->claim(cl->arg)) >= 0;) {
-                    (void)job((size_t)i);
-                    if (cl->done) cl->done(cl->arg, 1);
-                    count.fetch_add(1, std::memory_order_relaxed);
+    // par_iter().map(..).collect() (torrent.rs:724-740): each verdict goes
+    // straight into its slot, no channel; the split's threads take their
+    // pieces from the claim word instead of the counter.
+    std::atomic<int64_t> count{0};
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> ws;
+    for (int t = 0; t < std::max(1, threads); ++t)
+        ws.emplace_back([&] {
+            for (;;) {
+                int64_t i;
+                if (cl) {
+                    if ((i = cl->claim(cl->arg)) < 0) break;
+                } else {
+                    const size_t k = next.fetch_add(1, std::memory_order_relaxed);
+                    if (k >= n) break;
+                    i = (int64_t)k;
                 }
-            });
-        for (auto& w : ws) w.join();
-        taken = count.load();
-    } else {
-        run_pool(n, threads, job, ch);
-        std::memcpy(matched_out, result.data(), n);
-    }
+                (void)job((size_t)i);
+                if (cl && cl->done) cl->done(cl->arg, 1);
+                count.fetch_add(1, std::memory_order_relaxed);
+            }
+        });
+    for (auto& w : ws) w.join();
+    const int64_t taken = cl ? count.load() : 0;
+    if (!cl) std::memcpy(matched_out, result.data(), n);
     for (int fd : fds)
         if (fd >= 0) close(fd);
     return taken;

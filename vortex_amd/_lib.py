@@ -53,7 +53,7 @@ TUNING_EXPORTS = (
     "vx_synth_fill", "vx_sha1_device_uniform_variant", "vx_sha1_device_ragged_variant",
     "vx_tuning_zero_copy_plan", "vx_tuning_zero_copy_kernel", "vx_tuning_plan_ragged", "vx_tuning_chunk_schedule",
     "vx_tuning_fail_submit_after", "vx_tuning_fail_launch_after", "vx_tuning_verify_copy_stream", "vx_tuning_stage_huge",
-    "vx_tuning_clock_stamp",
+    "vx_tuning_split_rules", "vx_tuning_clock_stamp",
     "vx_tuning_wall_clock_khz", "vx_tuning_device_identity", "vx_tuning_split_take_tail",
     "vx_tuning_last_split",
 )
@@ -193,6 +193,7 @@ def _declare(L: ctypes.CDLL, tuning: bool = False) -> None:
             "vx_tuning_fail_launch_after": ([vp, c.c_int64], None),
             "vx_tuning_verify_copy_stream": ([vp, c.c_int], None),
             "vx_tuning_stage_huge": ([vp, c.c_int], None),
+            "vx_tuning_split_rules": ([vp, c.c_int, c.c_uint64], None),
             "vx_tuning_clock_stamp": ([vp, c.c_uint32, vp], c.c_int),
             "vx_tuning_wall_clock_khz": ([c.c_int], c.c_int),
             "vx_tuning_device_identity": ([c.c_int, c.c_char_p, c.c_size_t, c.c_char_p], c.c_int),

@@ -235,6 +235,13 @@ struct vx_ctx {
     // 45.2 GiB/s (its H2D copies 44-47 -> 49-50.5), cold 10.9 -> 14.2, median
     // of 7-9 alternating calls on one box.
     int stage_huge = 1;
+    // The split's rules for pieces of one chunk (vx_tuning_split_rules, test
+    // build): one_round 1 lets their groups keep claiming while the rates
+    // are cold and skips the tenth rule (0: the multi-round rules);
+    // round_cap > 0 caps their rounds' bytes (at no fewer than 1,024 lanes),
+    // 0: the slot's stage.
+    int split_one_round = 1;
+    uint64_t split_round_cap = 64ull << 20;
     hipEvent_t anchor_ev = nullptr;            // maps the rounds' GPU times onto the host clock
     uint64_t verify_t0_ns = 0;                 // the running re-verify call's start (steady clock)
 };
@@ -1774,7 +1781,9 @@ uint64_t split_take_tail(vx_split* s, uint64_t k, uint64_t expect = UINT64_MAX, 
 // the first group, which starts from earlier split calls on this context (or
 // the caller's per-thread rate, the PCIe rate and kChainBlock).  No later
 // group is formed until both sides have rates, and one only if it rides the
-// active lanes' rounds and shortens the predicted end by a tenth.  Alone on
+// active lanes' rounds and shortens the predicted end by a tenth — except
+// for pieces of one chunk, whose groups cost one round each: those keep the
+// first group's rule until the rates are in, and then only the model's.  Alone on
 // the split (engines 1) the engine's pieces are the contiguous tail
 // [*lowest, end); beside other engines, the groups it took.
 int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n, uint32_t pl, uint64_t total,
@@ -1790,7 +1799,7 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
     const uint64_t longest = std::max<uint64_t>(pl, last_len);
     const uint64_t pitch = align_up(std::min<uint64_t>(C, longest), vx_files::DirectIo::kBlock);
     const Slot& s0 = c->slots[0];
-    const uint64_t max_lanes = std::max<uint64_t>(1, std::min<uint64_t>(s0.cap, s0.arena_cap / pitch));
+    uint64_t max_lanes = std::max<uint64_t>(1, std::min<uint64_t>(s0.cap, s0.arena_cap / pitch));
     *lowest = end;
 
     struct Lane {
@@ -1821,6 +1830,13 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
         return v;
     };
     const std::vector<uint64_t> sched_plain = schedule(false), sched_ramp = schedule(true);
+    const bool one_round = c->split_one_round && sched_plain.size() == 1;  // every piece is one chunk (pl <= C)
+    // One-chunk pieces' rounds are whole groups: a smaller round starts the
+    // first copy sooner and ends the last kernel sooner (64 KiB pieces: 256 ->
+    // 64 MiB rounds, 50.5-52.5 -> 55.9-56.0 GiB/s; tools/split_rules_ab.py),
+    // but not below 1,024 lanes, whose kernels run one piece's chain each.
+    if (one_round && c->split_round_cap)
+        max_lanes = std::min(max_lanes, std::max<uint64_t>(1024, c->split_round_cap / pitch));
     struct Round {
         int si = -1;
         uint32_t m = 0;
@@ -1953,21 +1969,23 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             }
         }
         pool_samples.emplace_back(now, done);
-        // The first group is decided before the pool has a pace: a rate since
-        // the start is mostly its start-up, so it never goes below the rate the
-        // caller measured alone (an over-claim cannot be handed back; an
-        // under-claim is topped up once the rates are in).
-        if (mode == 1 && pool_threads > 0) p = std::max(p, pool_rate0);
-        // pieces the pool holds count half done
-        const double in_hand = 0.5 * ((double)(head - first) - (double)std::min<uint64_t>(done, head - first));
-        // The engine counts as measured once one copy is timed: its chain per
-        // block is a property of the kernel, known within a few % before any
-        // round of this call ends (kChainBlock), and waiting for a kernel end
-        // put the first measured group a whole round later.
         // A later group needs the pool's pace over a window (not its start-up)
         // and the engine's intake over two copies.
         *measured = in_n >= 2 && windowed;
-        if (!*measured && mode == 0) return 0;
+        // The first group is decided before the pool has a pace: a rate since
+        // the start is mostly its start-up, so it never goes below the rate the
+        // caller measured alone (an over-claim cannot be handed back; an
+        // under-claim is topped up once the rates are in).  Pieces that fit one
+        // round (a group costs one round, not a piece's whole chain) keep
+        // deciding so until the rates are in, rather than draining the pipeline.
+        const bool cold = mode == 1 || (mode == 0 && one_round && !*measured);
+        if (cold && pool_threads > 0) p = std::max(p, pool_rate0);
+        // pieces the pool holds count half done
+        const double in_hand = 0.5 * ((double)(head - first) - (double)std::min<uint64_t>(done, head - first));
+        // The engine's chain per block is a property of the kernel, known within
+        // a few % before any round of this call ends (kChainBlock); waiting for
+        // a kernel end put the first measured group a whole round later.
+        if (!*measured && !cold && mode == 0) return 0;
         if (windowed) last_p = p;
         const double rin = in_n >= 2 && in_ms > 0 ? in_bytes / (in_ms * 1e-3)
                            : c->split_rin > 0     ? c->split_rin
@@ -2042,8 +2060,9 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             }
         }
 
-        // and a later group must shorten the predicted end by a tenth
-        if (mode == 0 && lo > 0 &&
+        // and a later group must shorten the predicted end by a tenth (a group
+        // of one-round pieces risks one round, and is a small share of the end)
+        if (mode == 0 && !one_round && lo > 0 &&
             std::max(t_engine(lo), t_pool(lo)) > 0.9 * std::max(t_engine(0), t_pool(0)))
             lo = 0;
         c->last_split.push_back(vx_ctx::SplitDecision{
@@ -3034,6 +3053,11 @@ void vx_tuning_fail_launch_after(vx_ctx* c, int64_t k) {
 }
 void vx_tuning_verify_copy_stream(vx_ctx* c, int mode) {
     if (c) c->verify_copy_stream = mode ? 1 : 0;
+}
+void vx_tuning_split_rules(vx_ctx* c, int one_round, uint64_t round_cap) {
+    if (!c) return;
+    c->split_one_round = one_round ? 1 : 0;
+    c->split_round_cap = round_cap;
 }
 void vx_tuning_stage_huge(vx_ctx* c, int on) {
     if (!c) return;
