@@ -258,3 +258,36 @@ def test_split_stats_count_the_engines_pieces_only(built, gpu, tmp_path):
         assert bad == len(io_err) == st["io_errors"]
         assert st["pieces_completed"] == n - b
         assert st["pieces_mismatched"] == sum(1 for i in range(b, n) if not want[i]) - len(io_err)
+
+
+@pytest.mark.parametrize("one_round,cap", [(1, 64 << 20), (1, 0), (0, 0)])
+def test_split_one_chunk_pieces(built, gpu, tmp_path, one_round, cap):
+    """Pieces of one chunk (64 KiB, 4,000 of them over two files, a piece
+    across the file boundary, damaged pieces near each end) under each rule
+    set for them (vx_tuning_split_rules: the default 64 MiB rounds, uncapped,
+    the multi-round rules): every verdict is the pool restatement's, and with
+    the cap no round carries more than 1,024 lanes."""
+    from vortex_amd.hash_pool import HashPool
+
+    pl = 64 << 10
+    sizes = [2500 * pl + 4321, 1500 * pl - 4321 - 999]
+    paths, sizes, exp = _files(tmp_path, pl, sizes, 71)
+    n = len(exp) // 20
+    for p, off in ((paths[0], 5 * pl + 3), (paths[1], 1400 * pl + 7)):
+        with open(p, "r+b") as f:
+            f.seek(off)
+            b = f.read(1)
+            f.seek(off)
+            f.write(bytes([b[0] ^ 0x42]))
+    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
+    with HashPool(pl, slots=4, slot_bytes=512 << 20, batch_pieces=4096, hooks=True) as pool:
+        pool.lib.vx_tuning_split_rules(pool._h, one_round, cap)
+        try:
+            for rep in range(3):
+                sp, taken, bad = _run_split(pool, paths, sizes, pl, exp, 0, n, 4, io_threads=4)
+                assert sp.verdicts() == want and taken == sp.boundary, (rep, sp.boundary)
+                assert sp.boundary < n  # the engine took part
+                if cap:
+                    assert max(r["lanes"] for r in pool.last_verify_rounds()) <= 1024
+        finally:
+            pool.lib.vx_tuning_split_rules(pool._h, 1, 64 << 20)
