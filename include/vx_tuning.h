@@ -59,8 +59,9 @@ void vx_tuning_verify_copy_stream(struct vx_ctx* ctx, int mode);
 void vx_tuning_stage_huge(struct vx_ctx* ctx, int on);
 /* A/B of the split's rules for pieces of one chunk (vx_verify_files_split,
  * DESIGN.md §6.6): one_round = 1 (the default) lets their groups keep the
- * first group's rule until the rates are in and skips the tenth rule, 0 gives
- * them the multi-round pieces' rules; round_cap > 0 (default 64 MiB) caps
+ * first group's rule until the rates are in, skips the tenth rule and reads
+ * runs of them with one pread, 2 does the same piece by piece, 0 gives them
+ * the multi-round pieces' rules; round_cap > 0 (default 64 MiB) caps
  * their rounds at that many bytes but no fewer than 1,024 lanes, 0 gives them
  * the slot's whole stage. */
 void vx_tuning_split_rules(struct vx_ctx* ctx, int one_round, uint64_t round_cap);

@@ -4,7 +4,8 @@
 vx_tuning_split_rules: `old` gives one-chunk pieces the multi-round rules (no
 group until both sides have rates, the tenth rule), `new` lets them keep the
 first group's rule while cold and skips the tenth rule, `capN` adds a cap of
-N MiB (at least 1,024 lanes) on their rounds, `auto` is the default (cap64).
+N MiB (at least 1,024 lanes) on their rounds, `auto` is the default (cap64),
+`perpiece` the default reading piece by piece instead of in runs.
 For each piece length this writes a ~2 GiB file of synthetic pieces, warms it, and alternates the variants' balanced splits
 (bench.balanced_call) with the engine alone at the split's readers, every
 verdict checked; prints the medians.
@@ -33,6 +34,8 @@ def rules(name):
         return 1, 0
     if name == "auto":  # the default: 64 MiB, at least 1,024 lanes
         return 1, 64 << 20
+    if name == "perpiece":  # the default, reading piece by piece
+        return 2, 64 << 20
     return 1, int(name[3:]) << 20
 
 

@@ -237,7 +237,8 @@ struct vx_ctx {
     int stage_huge = 1;
     // The split's rules for pieces of one chunk (vx_tuning_split_rules, test
     // build): one_round 1 lets their groups keep claiming while the rates
-    // are cold and skips the tenth rule (0: the multi-round rules);
+    // are cold and skips the tenth rule (0: the multi-round rules; 2: as 1,
+    // reading piece by piece instead of in runs);
     // round_cap > 0 caps their rounds' bytes (at no fewer than 1,024 lanes),
     // 0: the slot's stage.
     int split_one_round = 1;
@@ -2126,9 +2127,15 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
                                                        align_up(max_chunk, vx_files::DirectIo::kBlock));
                 uint32_t m = 0;
                 std::vector<Lane> keep;
+                // one-chunk pieces are whole pieces in increasing order: runs of
+                // them inside one file go out as one pread (as in verify_whole)
+                vx_files::Runs runs = rd.runs(one_round && c->split_one_round != 2 ? 4ull << 20 : 0);
                 for (const Lane& l : lanes) {
                     const uint64_t L = plen(l.piece), clen = chunk_len(L, l.a, l.ramp);
-                    it.push_back(vx_files::ReadItem{s.h_stage + (uint64_t)m * rp, l.piece, l.a, clen});
+                    if (one_round)
+                        runs.add(it, s.h_stage + (uint64_t)m * rp, l.piece, clen);
+                    else
+                        it.push_back(vx_files::ReadItem{s.h_stage + (uint64_t)m * rp, l.piece, l.a, clen});
                     s.h_offsets[m] = (uint64_t)m * rp;
                     s.h_lens[m] = (uint32_t)clen;
                     s.h_pidx[m] = (uint32_t)(l.piece - first);
@@ -3056,7 +3063,7 @@ void vx_tuning_verify_copy_stream(vx_ctx* c, int mode) {
 }
 void vx_tuning_split_rules(vx_ctx* c, int one_round, uint64_t round_cap) {
     if (!c) return;
-    c->split_one_round = one_round ? 1 : 0;
+    c->split_one_round = one_round == 2 ? 2 : one_round ? 1 : 0;
     c->split_round_cap = round_cap;
 }
 void vx_tuning_stage_huge(vx_ctx* c, int on) {
