@@ -63,8 +63,9 @@ void vx_tuning_stage_huge(struct vx_ctx* ctx, int on);
  * runs of them with one pread, 2 does the same piece by piece, 0 gives them
  * the multi-round pieces' rules; round_cap > 0 (default 64 MiB) caps
  * their rounds at that many bytes but no fewer than 1,024 lanes, 0 gives them
- * the slot's whole stage. */
-void vx_tuning_split_rules(struct vx_ctx* ctx, int one_round, uint64_t round_cap);
+ * the slot's whole stage.  lag = 1 (the default) adds the learned lag to the
+ * first group's T_engine, 0 keeps learning it without adding it. */
+void vx_tuning_split_rules(struct vx_ctx* ctx, int one_round, uint64_t round_cap, int lag);
 /* The kernel vx_sha1_device_ragged_hint runs for a batch of n pieces whose
  * longest is max_len bytes, total_len bytes in all: 1 = lane, 2 = split,
  * 5 = split with one pair per CU (host-only). */

@@ -222,6 +222,14 @@ struct vx_ctx {
     // (B/s, first copy start to last copy end), the kernel's chain per block,
     // and the pool's bytes/s per thread beside the engine (0 = none yet).
     double split_rin = 0, split_bns = 0, split_pool_thread_rate = 0;
+    // How much later the engine's last kernel ended than the first group's
+    // T_engine said, in calls where the first group was the engine's only one
+    // (the readers' start-up and the kernels trailing the copies, which the
+    // round model leaves out), averaged the same way; the next first group's
+    // T_engine adds it.
+    double split_lag_s = 0;
+    uint32_t split_lag_n = 0;
+    int split_lag_on = 1;  // 0: learned, not applied (vx_tuning_split_rules)
     // The file re-verify's chunk rounds put every H2D on this one stream (high
     // priority: its own hardware queue) and only kernels on the slot streams,
     // so no copy ever sits behind a kernel.  Created on first
@@ -1780,7 +1788,9 @@ uint64_t split_take_tail(vx_split* s, uint64_t k, uint64_t expect = UINT64_MAX, 
 // start to last copy end), the chain per 64-byte block from the kernel
 // events, the pool's pace over its last 4 ms of vx_split_done — except for
 // the first group, which starts from earlier split calls on this context (or
-// the caller's per-thread rate, the PCIe rate and kChainBlock).  No later
+// the caller's per-thread rate, the PCIe rate and kChainBlock); its T_engine
+// adds the lag earlier calls' single groups ended behind their prediction
+// (the readers' start-up and the kernels trailing the copies).  No later
 // group is formed until both sides have rates, and one only if it rides the
 // active lanes' rounds and shortens the predicted end by a tenth — except
 // for pieces of one chunk, whose groups cost one round each: those keep the
@@ -1892,6 +1902,10 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
                                                              : 2.2e9;
     const double pool_rate0 = pool_threads * thread_rate0 / (double)pl;
     double last_p = 0;  // the pool's pace at the last decision
+    // the first group's predicted end (call clock, ms, without the learned
+    // lag) and span, and whether any later group joined: the lag's sample
+    double first_end_ms = -1, first_span_ms = 0, lag_used = 0;
+    bool later_group = false;
 
     // Fold newly finished rounds into the copy and chain rates (events are
     // queried, never waited for).
@@ -2022,6 +2036,7 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             }
         }
         const std::vector<uint64_t>& js = mode == 1 ? sched_ramp : sched_plain;
+        lag_used = mode == 1 && c->split_lag_on ? c->split_lag_s : 0.0;
         // Each round costs max(its bytes over the intake, its chain), copies
         // overlapping the previous round's kernel; after the last copy, the
         // last kernel's chain; before the first, the first round's read.
@@ -2036,7 +2051,7 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
                 if (j && r < js.size()) b += (double)j * (double)js[r], k = std::max(k, js[r]);
                 if (b > 0) t += round_s(b, k) + (r == 0 && first_read ? b / rin : 0.0), k_end = k;
             }
-            return t + (double)((k_end + 63) / 64) * bns * 1e-9;
+            return t + (double)((k_end + 63) / 64) * bns * 1e-9 + lag_used;
         };
         auto t_pool = [&](uint64_t j) {  // the others take an equal share each
             const double left = (double)unclaimed - (double)(engines * j);
@@ -2118,6 +2133,13 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
                         mine.emplace_back(lo, old);
                     for (uint64_t i = lo; i < old; ++i) lanes.push_back(Lane{i, 0, !formed_any});
                     *lowest = std::min(*lowest, lo);
+                    const vx_ctx::SplitDecision& d = c->last_split.back();
+                    if (mode == 1) {
+                        first_span_ms = d.t_engine_ms - lag_used * 1e3;
+                        first_end_ms = d.t_ms + first_span_ms;
+                    } else if (lo < old) {
+                        later_group = true;
+                    }
                 }
                 // lanes sit one round pitch apart: the round's longest chunk,
                 // 4 KiB aligned for O_DIRECT (ramp rounds copy no gaps)
@@ -2276,6 +2298,13 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             mean(c->split_bns, block_ns[block_ns.size() / 2]);
         }
         if (last_p > 0 && pool_threads > 0) mean(c->split_pool_thread_rate, last_p * (double)pl / pool_threads);
+        // the lag: the last kernel's end against the first group's prediction
+        double end_ms = -1;
+        for (const auto& r : c->last_rounds) end_ms = std::max(end_ms, r.kernel_end_ms);
+        if (anchored && !later_group && first_end_ms > 0 && end_ms > 0 && first_span_ms > 0) {
+            const double v = std::clamp(end_ms - first_end_ms, -0.25 * first_span_ms, 0.5 * first_span_ms) * 1e-3;
+            c->split_lag_s = c->split_lag_n++ ? 0.5 * (c->split_lag_s + v) : v;
+        }
     }
     fv.done = 0;
     for (const auto& r : rows) fv.done += r.second - r.first;
@@ -3061,8 +3090,9 @@ void vx_tuning_fail_launch_after(vx_ctx* c, int64_t k) {
 void vx_tuning_verify_copy_stream(vx_ctx* c, int mode) {
     if (c) c->verify_copy_stream = mode ? 1 : 0;
 }
-void vx_tuning_split_rules(vx_ctx* c, int one_round, uint64_t round_cap) {
+void vx_tuning_split_rules(vx_ctx* c, int one_round, uint64_t round_cap, int lag) {
     if (!c) return;
+    c->split_lag_on = lag ? 1 : 0;
     c->split_one_round = one_round == 2 ? 2 : one_round ? 1 : 0;
     c->split_round_cap = round_cap;
 }
