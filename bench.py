@@ -673,7 +673,7 @@ def balanced_call(pool, paths: list, lens: list, n: int, pl: int, exp: bytes, io
             "boundary": sp.boundary, "pool_pieces": res["taken"], "matched": got}
 
 
-def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 7):
+def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 11):
     """BASELINE config 5: full re-verify of a torrent's data from disk with
     the linux-mint geometry (cli/linux-mint.torrent: 2,907,832,320 B, 2 MiB
     pieces, last 1,179,648 B) through vx_verify_files (pread into pinned

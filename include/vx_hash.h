@@ -329,10 +329,11 @@ int64_t vx_verify_files_range(vx_ctx* ctx, const char* const* paths, const uint6
  * this call (the pool's finished pieces per second through vx_split_done;
  * its own copy, read and per-block chain rates from the rounds' GPU events),
  * and takes the group of pieces that keeps the two finish times equal.
- * Until the first measurements exist it starts on half of what the cold-start
- * rates (cpu_threads x cpu_thread_rate, the PCIe rate) would give it, since a
- * claim cannot be handed back.  The caller owns the struct; it may live on
- * the stack of the thread that starts both sides. */
+ * Its first group, before anything is measured, comes from the previous
+ * split calls on the same context (their rates, and how far their finish
+ * times strayed from the prediction), else from cpu_threads x
+ * cpu_thread_rate and the PCIe rate.  The caller owns the struct; it may live
+ * on the stack of the thread that starts both sides. */
 typedef struct vx_split {
     uint64_t word;          /* head (low 32 bits) | stop (high 32): [head, stop) is unclaimed          */
     uint64_t pool_done;     /* pieces the pool finished (vx_split_done)                                */
@@ -342,6 +343,7 @@ typedef struct vx_split {
     uint32_t cpu_threads;   /* the pool's threads (0 = no pool: the engine takes every piece)          */
     uint32_t engines;       /* engines claiming at once (0 or 1: one; vx_verify_files_split_multi sets it) */
     double cpu_thread_rate; /* the pool's bytes/s per thread alone (cold start only; 0 = 2.2e9, SHA-NI) */
+    uint64_t pool_last_ns;  /* steady clock at the pool's latest vx_split_done (when the pool finished)  */
 } vx_split;
 /* Pieces [first, end) unclaimed; end - first < 2^32 and end < 2^32. */
 int vx_split_init(vx_split* s, uint64_t first, uint64_t end, uint32_t cpu_threads, double cpu_thread_rate);

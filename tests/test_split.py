@@ -40,16 +40,17 @@ def test_split_struct_matches_header(tmp_path):
 
     src = tmp_path / "s.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "vx_hash.h"\n'
-                   'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu\\n", sizeof(vx_split),'
+                   'int main(void){printf("%zu %zu %zu %zu %zu %zu %zu %zu\\n", sizeof(vx_split),'
                    ' offsetof(vx_split, pool_done), offsetof(vx_split, start_ns), offsetof(vx_split, first),'
-                   ' offsetof(vx_split, end), offsetof(vx_split, cpu_threads), offsetof(vx_split, cpu_thread_rate));'
+                   ' offsetof(vx_split, end), offsetof(vx_split, cpu_threads), offsetof(vx_split, cpu_thread_rate),'
+                   ' offsetof(vx_split, pool_last_ns));'
                    'return 0;}\n')
     exe = tmp_path / "s"
     subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     S = _lib.vx_split
     assert got == [ctypes.sizeof(S), S.pool_done.offset, S.start_ns.offset, S.first.offset, S.end.offset,
-                   S.cpu_threads.offset, S.cpu_thread_rate.offset]
+                   S.cpu_threads.offset, S.cpu_thread_rate.offset, S.pool_last_ns.offset]
 
 
 def test_split_init_validation():
@@ -82,6 +83,7 @@ def test_pool_alone_takes_every_piece(tmp_path):
     taken = oracle.pool_verify_files_claim(paths, [os.path.getsize(p) for p in paths], pl, exp, 3, sp.claim_fn,
                                            sp.done_fn, sp.arg, 0, sp.matched)
     assert taken == n and sp.pool_done == n and sp.boundary == n
+    assert sp.s.start_ns <= sp.s.pool_last_ns  # the pool's last verdict time (the engine's balance sample)
     assert sp.verdicts() == oracle.pool_verify_files(paths, [os.path.getsize(p) for p in paths], pl, exp)
 
 

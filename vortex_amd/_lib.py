@@ -124,7 +124,8 @@ class vx_split(ctypes.Structure):
     """The split's claim word and the pool's progress (include/vx_hash.h)."""
     _fields_ = [("word", ctypes.c_uint64), ("pool_done", ctypes.c_uint64), ("start_ns", ctypes.c_uint64),
                 ("first", ctypes.c_uint64), ("end", ctypes.c_uint64), ("cpu_threads", ctypes.c_uint32),
-                ("engines", ctypes.c_uint32), ("cpu_thread_rate", ctypes.c_double)]
+                ("engines", ctypes.c_uint32), ("cpu_thread_rate", ctypes.c_double),
+                ("pool_last_ns", ctypes.c_uint64)]
 
 
 _lib = None

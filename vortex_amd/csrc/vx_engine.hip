@@ -223,10 +223,11 @@ struct vx_ctx {
     // and the pool's bytes/s per thread beside the engine (0 = none yet).
     double split_rin = 0, split_bns = 0, split_pool_thread_rate = 0;
     // How much later the engine's last kernel ended than the first group's
-    // T_engine said, in calls where the first group was the engine's only one
-    // (the readers' start-up and the kernels trailing the copies, which the
-    // round model leaves out), averaged the same way; the next first group's
-    // T_engine adds it.
+    // T_engine said, less the same for the pool's last verdict and T_pool, in
+    // calls where the first group was the engine's only one (the readers'
+    // start-up and the kernels trailing the copies, which the round model
+    // leaves out), averaged the same way; the next first group's T_engine
+    // adds it.
     double split_lag_s = 0;
     uint32_t split_lag_n = 0;
     int split_lag_on = 1;  // 0: learned, not applied (vx_tuning_split_rules)
@@ -1902,9 +1903,10 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
                                                              : 2.2e9;
     const double pool_rate0 = pool_threads * thread_rate0 / (double)pl;
     double last_p = 0;  // the pool's pace at the last decision
-    // the first group's predicted end (call clock, ms, without the learned
-    // lag) and span, and whether any later group joined: the lag's sample
-    double first_end_ms = -1, first_span_ms = 0, lag_used = 0;
+    // the first group's predicted ends (call clock, ms; the engine's without
+    // the learned lag) and the engine's span, and whether any later group
+    // joined: the lag's sample
+    double first_end_ms = -1, first_pool_end_ms = -1, first_span_ms = 0, lag_used = 0;
     bool later_group = false;
 
     // Fold newly finished rounds into the copy and chain rates (events are
@@ -2137,6 +2139,7 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
                     if (mode == 1) {
                         first_span_ms = d.t_engine_ms - lag_used * 1e3;
                         first_end_ms = d.t_ms + first_span_ms;
+                        first_pool_end_ms = d.t_ms + d.t_pool_ms;
                     } else if (lo < old) {
                         later_group = true;
                     }
@@ -2298,12 +2301,34 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             mean(c->split_bns, block_ns[block_ns.size() / 2]);
         }
         if (last_p > 0 && pool_threads > 0) mean(c->split_pool_thread_rate, last_p * (double)pl / pool_threads);
-        // the lag: the last kernel's end against the first group's prediction
+        // The lag: how much later than predicted the engine's last kernel
+        // ended, less how much later than predicted the pool's last verdict
+        // came (vx_split.pool_last_ns; a pool still working is estimated from
+        // its pace), both against the first group's decision.
         double end_ms = -1;
         for (const auto& r : c->last_rounds) end_ms = std::max(end_ms, r.kernel_end_ms);
-        if (anchored && !later_group && first_end_ms > 0 && end_ms > 0 && first_span_ms > 0) {
-            const double v = std::clamp(end_ms - first_end_ms, -0.25 * first_span_ms, 0.5 * first_span_ms) * 1e-3;
-            c->split_lag_s = c->split_lag_n++ ? 0.5 * (c->split_lag_s + v) : v;
+        if (anchored && !later_group && engines == 1 && first_end_ms > 0 && end_ms > 0 && first_span_ms > 0) {
+            double err = end_ms - first_end_ms;
+            bool ok = true;
+            if (pool_threads > 0) {
+                const uint64_t w = __atomic_load_n(&sp->word, __ATOMIC_ACQUIRE);
+                const uint64_t head = w & 0xffffffffull, stop = w >> 32;
+                const uint64_t done = __atomic_load_n(&sp->pool_done, __ATOMIC_ACQUIRE);
+                const uint64_t last_ns = __atomic_load_n(&sp->pool_last_ns, __ATOMIC_ACQUIRE);
+                const uint64_t claimed = head - first, unclaimed = stop > head ? stop - head : 0;
+                double pool_end_ms = -1;
+                if (!unclaimed && done >= claimed && last_ns)
+                    pool_end_ms = ((double)last_ns - (double)c->verify_t0_ns) * 1e-6;
+                else if (last_p > 0)
+                    pool_end_ms = rel_ms(vx_files::Readers::now_ns()) +
+                                  (0.5 * (double)(claimed - std::min(done, claimed)) + (double)unclaimed) / last_p * 1e3;
+                ok = pool_end_ms > 0 && first_pool_end_ms > 0;
+                err -= pool_end_ms - first_pool_end_ms;
+            }
+            if (ok) {
+                const double v = std::clamp(err, -0.25 * first_span_ms, 0.5 * first_span_ms) * 1e-3;
+                c->split_lag_s = c->split_lag_n++ ? 0.5 * (c->split_lag_s + v) : v;
+            }
         }
     }
     fv.done = 0;
@@ -2720,7 +2745,15 @@ int64_t vx_split_claim(vx_split* s) {
 }
 
 void vx_split_done(vx_split* s, uint64_t pieces) {
-    if (s) __atomic_fetch_add(&s->pool_done, pieces, __ATOMIC_RELEASE);
+    if (!s) return;
+    // the latest verdict's time (a later one never moves it back), published
+    // with the count
+    const uint64_t t = vx_files::Readers::now_ns();
+    uint64_t was = __atomic_load_n(&s->pool_last_ns, __ATOMIC_RELAXED);
+    while (was < t &&
+           !__atomic_compare_exchange_n(&s->pool_last_ns, &was, t, true, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+    }
+    __atomic_fetch_add(&s->pool_done, pieces, __ATOMIC_RELEASE);
 }
 
 uint64_t vx_split_boundary(const vx_split* s) {
