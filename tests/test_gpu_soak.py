@@ -174,7 +174,7 @@ def test_soak_split_engines(built, gpu, tmp_path):
     t_end = time.time() + float(os.environ.get("VX_SOAK_SECONDS", "10"))
     calls = failed = 0
     while time.time() < t_end:
-        pl = rng.choice([64 << 10, 256 << 10, 1 << 20, 2 << 20])
+        pl = rng.choice([16 << 10, 64 << 10, 256 << 10, 1 << 20, 2 << 20])
         d = tmp_path / f"s{calls}"
         d.mkdir()
         paths, sizes, exp = _torrent(str(d), rng, pl, 1000 + calls)
