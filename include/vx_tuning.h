@@ -64,8 +64,10 @@ void vx_tuning_stage_huge(struct vx_ctx* ctx, int on);
  * the multi-round pieces' rules; round_cap > 0 (default 64 MiB) caps
  * their rounds at that many bytes but no fewer than 1,024 lanes, 0 gives them
  * the slot's whole stage.  lag = 1 (the default) adds the learned lag to the
- * first group's T_engine, 0 keeps learning it without adding it. */
-void vx_tuning_split_rules(struct vx_ctx* ctx, int one_round, uint64_t round_cap, int lag);
+ * first group's T_engine, 0 keeps learning it without adding it.  learn = 1
+ * (the default) starts each call from the median of the last five calls'
+ * figures, 0 from their running mean (each call weighted 1/2). */
+void vx_tuning_split_rules(struct vx_ctx* ctx, int one_round, uint64_t round_cap, int lag, int learn);
 /* The kernel vx_sha1_device_ragged_hint runs for a batch of n pieces whose
  * longest is max_len bytes, total_len bytes in all: 1 = lane, 2 = split,
  * 5 = split with one pair per CU (host-only). */

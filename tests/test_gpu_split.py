@@ -281,7 +281,7 @@ def test_split_one_chunk_pieces(built, gpu, tmp_path, one_round, cap):
             f.write(bytes([b[0] ^ 0x42]))
     want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
     with HashPool(pl, slots=4, slot_bytes=512 << 20, batch_pieces=4096, hooks=True) as pool:
-        pool.lib.vx_tuning_split_rules(pool._h, one_round, cap, 1)
+        pool.lib.vx_tuning_split_rules(pool._h, one_round, cap, 1, 1)
         try:
             for rep in range(3):
                 sp, taken, bad = _run_split(pool, paths, sizes, pl, exp, 0, n, 4, io_threads=4)
@@ -290,4 +290,4 @@ def test_split_one_chunk_pieces(built, gpu, tmp_path, one_round, cap):
                 if cap:
                     assert max(r["lanes"] for r in pool.last_verify_rounds()) <= 1024
         finally:
-            pool.lib.vx_tuning_split_rules(pool._h, 1, 64 << 20, 1)
+            pool.lib.vx_tuning_split_rules(pool._h, 1, 64 << 20, 1, 1)

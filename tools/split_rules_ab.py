@@ -6,7 +6,8 @@ group until both sides have rates, the tenth rule), `new` lets them keep the
 first group's rule while cold and skips the tenth rule, `capN` adds a cap of
 N MiB (at least 1,024 lanes) on their rounds, `auto` is the default (cap64),
 `perpiece` the default reading piece by piece instead of in runs, `nolag` the
-default without the learned lag on the first group.
+default without the learned lag on the first group, `ewma` the default
+learning by running mean instead of the median of the last five calls.
 For each piece length this writes a ~2 GiB file of synthetic pieces, warms it, and alternates the variants' balanced splits
 (bench.balanced_call) with the engine alone at the split's readers, every
 verdict checked; prints the medians.
@@ -30,16 +31,18 @@ from vortex_amd.hash_pool import HashPool  # noqa: E402
 
 def rules(name):
     if name == "old":
-        return 0, 0, 1
+        return 0, 0, 1, 1
     if name == "new":
-        return 1, 0, 1
+        return 1, 0, 1, 1
     if name == "auto":  # the default: 64 MiB, at least 1,024 lanes
-        return 1, 64 << 20, 1
+        return 1, 64 << 20, 1, 1
     if name == "perpiece":  # the default, reading piece by piece
-        return 2, 64 << 20, 1
+        return 2, 64 << 20, 1, 1
     if name == "nolag":  # the default, the first group without the learned lag
-        return 1, 64 << 20, 0
-    return 1, int(name[3:]) << 20, 1
+        return 1, 64 << 20, 0, 1
+    if name == "ewma":  # the default, learning by running mean instead of the median of 5
+        return 1, 64 << 20, 1, 0
+    return 1, int(name[3:]) << 20, 1, 1
 
 
 def main():
@@ -67,7 +70,7 @@ def main():
             with HashPool(pl, slots=4, slot_bytes=512 << 20, batch_pieces=4096, hooks=True) as pool:
                 pool.verify_files([path], [total], pl, exp, io_threads=io_t)
                 for r in range(reps):
-                    pool.lib.vx_tuning_split_rules(pool._h, 1, 64 << 20, 1)
+                    pool.lib.vx_tuning_split_rules(pool._h, 1, 64 << 20, 1, 1)
                     t0 = time.perf_counter()
                     _, bad = pool.verify_files([path], [total], pl, exp, io_threads=io_t)
                     runs["engine"].append(time.perf_counter() - t0)
@@ -78,7 +81,7 @@ def main():
                         assert c["ok"], f"{kib} KiB {v}: the split's verdicts differ"
                         runs[v].append(c["s"])
                         bounds[v].append(c["boundary"])
-                pool.lib.vx_tuning_split_rules(pool._h, 1, 64 << 20, 1)
+                pool.lib.vx_tuning_split_rules(pool._h, 1, 64 << 20, 1, 1)
             g = {k: round(total / med(v) / (1 << 30), 2) for k, v in runs.items()}
             res["geoms"][f"{kib}K"] = {"pieces": n, "GiBps": g, "boundaries": bounds,
                                       "s_runs": {k: [round(x, 4) for x in v] for k, v in runs.items()}}

@@ -194,7 +194,7 @@ def _declare(L: ctypes.CDLL, tuning: bool = False) -> None:
             "vx_tuning_fail_launch_after": ([vp, c.c_int64], None),
             "vx_tuning_verify_copy_stream": ([vp, c.c_int], None),
             "vx_tuning_stage_huge": ([vp, c.c_int], None),
-            "vx_tuning_split_rules": ([vp, c.c_int, c.c_uint64, c.c_int], None),
+            "vx_tuning_split_rules": ([vp, c.c_int, c.c_uint64, c.c_int, c.c_int], None),
             "vx_tuning_clock_stamp": ([vp, c.c_uint32, vp], c.c_int),
             "vx_tuning_wall_clock_khz": ([c.c_int], c.c_int),
             "vx_tuning_device_identity": ([c.c_int, c.c_char_p, c.c_size_t, c.c_char_p], c.c_int),

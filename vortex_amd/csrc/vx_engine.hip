@@ -217,19 +217,41 @@ struct vx_ctx {
         uint32_t mode, measured;
     };
     std::vector<SplitDecision> last_split;
-    // What earlier split calls measured (a running mean over calls, each call
-    // weighted 1/2), the next call's cold start: the engine's copy intake
+    // What earlier split calls measured, the next call's cold start: the
+    // engine's copy intake
     // (B/s, first copy start to last copy end), the kernel's chain per block,
     // and the pool's bytes/s per thread beside the engine (0 = none yet).
-    double split_rin = 0, split_bns = 0, split_pool_thread_rate = 0;
+    // Each keeps the last kLearn calls' samples: the next call uses their
+    // median (split_learn 1, default), so one call slowed by a host stall
+    // does not move the next call's first group; split_learn 0 (test build)
+    // uses the running mean instead (each call weighted 1/2).
+    struct Learned {
+        static constexpr uint32_t kLearn = 5;
+        double ring[kLearn] = {}, mean = 0;
+        uint32_t n = 0;
+        void add(double x) {
+            mean = n ? 0.5 * (mean + x) : x;
+            ring[n++ % kLearn] = x;
+        }
+        bool any() const { return n > 0; }
+        double get(int median) const {
+            if (!median) return mean;
+            double v[kLearn];
+            const uint32_t k = std::min(n, kLearn);
+            std::copy(ring, ring + k, v);
+            std::sort(v, v + k);
+            return k % 2 ? v[k / 2] : 0.5 * (v[k / 2 - 1] + v[k / 2]);
+        }
+    };
+    Learned split_rin, split_bns, split_pool_thread_rate;
+    int split_learn = 1;
     // How much later the engine's last kernel ended than the first group's
     // T_engine said, less the same for the pool's last verdict and T_pool, in
     // calls where the first group was the engine's only one (the readers'
     // start-up and the kernels trailing the copies, which the round model
-    // leaves out), averaged the same way; the next first group's T_engine
-    // adds it.
-    double split_lag_s = 0;
-    uint32_t split_lag_n = 0;
+    // leaves out), kept the same way; the next first group's T_engine adds
+    // it.
+    Learned split_lag;
     int split_lag_on = 1;  // 0: learned, not applied (vx_tuning_split_rules)
     // The file re-verify's chunk rounds put every H2D on this one stream (high
     // priority: its own hardware queue) and only kernels on the slot streams,
@@ -1898,7 +1920,7 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
     std::vector<std::pair<uint64_t, uint64_t>> mine;  // this engine's claims, [lo, hi), in claim order
     std::vector<std::pair<uint64_t, uint64_t>> pool_samples;  // (steady ns, pool_done) at each decision
     constexpr uint64_t kPoolWindowNs = 4000000;              // the pool's pace: its last 4 ms
-    const double thread_rate0 = c->split_pool_thread_rate > 0 ? c->split_pool_thread_rate
+    const double thread_rate0 = c->split_pool_thread_rate.any() ? c->split_pool_thread_rate.get(c->split_learn)
                                 : sp->cpu_thread_rate > 0    ? sp->cpu_thread_rate
                                                              : 2.2e9;
     const double pool_rate0 = pool_threads * thread_rate0 / (double)pl;
@@ -2005,9 +2027,9 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
         if (!*measured && !cold && mode == 0) return 0;
         if (windowed) last_p = p;
         const double rin = in_n >= 2 && in_ms > 0 ? in_bytes / (in_ms * 1e-3)
-                           : c->split_rin > 0     ? c->split_rin
+                           : c->split_rin.any()   ? c->split_rin.get(c->split_learn)
                                                   : kPcieRate;
-        double bns = c->split_bns > 0 ? c->split_bns : kChainBlock * 1e9;
+        double bns = c->split_bns.any() ? c->split_bns.get(c->split_learn) : kChainBlock * 1e9;
         if (!block_ns.empty()) {
             std::vector<double> b = block_ns;
             std::nth_element(b.begin(), b.begin() + b.size() / 2, b.end());
@@ -2038,7 +2060,7 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             }
         }
         const std::vector<uint64_t>& js = mode == 1 ? sched_ramp : sched_plain;
-        lag_used = mode == 1 && c->split_lag_on ? c->split_lag_s : 0.0;
+        lag_used = mode == 1 && c->split_lag_on && c->split_lag.any() ? c->split_lag.get(c->split_learn) : 0.0;
         // Each round costs max(its bytes over the intake, its chain), copies
         // overlapping the previous round's kernel; after the last copy, the
         // last kernel's chain; before the first, the first round's read.
@@ -2280,9 +2302,8 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             for (uint64_t i = r.first; i < r.second; ++i)
                 if (fv.bad[i]) fv.matched_out[i] = 0;
         // the next split call's cold start (this host, this load): this
-        // call's figures, averaged with the earlier calls' at 1/2
+        // call's figures join the last calls' (Learned)
         measure();
-        auto mean = [](double& m, double v) { m = m > 0 ? 0.5 * (m + v) : v; };
         // the steady-state intake: the full-chunk rounds' bytes over the time
         // from the copy before the first of them to the last one's end (the
         // ramps' short rounds and the chain-bound tail would understate it,
@@ -2294,13 +2315,13 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             double bytes = 0;
             for (size_t k = a + 1; k <= b && a < copy_ends.size(); ++k) bytes += (double)copy_ends[k].bytes;
             const double ms = a < b ? copy_ends[b].end_ms - copy_ends[a].end_ms : 0.0;
-            if (ms > 0 && bytes > 0) mean(c->split_rin, bytes / (ms * 1e-3));
+            if (ms > 0 && bytes > 0) c->split_rin.add(bytes / (ms * 1e-3));
         }
         if (!block_ns.empty()) {
             std::nth_element(block_ns.begin(), block_ns.begin() + block_ns.size() / 2, block_ns.end());
-            mean(c->split_bns, block_ns[block_ns.size() / 2]);
+            c->split_bns.add(block_ns[block_ns.size() / 2]);
         }
-        if (last_p > 0 && pool_threads > 0) mean(c->split_pool_thread_rate, last_p * (double)pl / pool_threads);
+        if (last_p > 0 && pool_threads > 0) c->split_pool_thread_rate.add(last_p * (double)pl / pool_threads);
         // The lag: how much later than predicted the engine's last kernel
         // ended, less how much later than predicted the pool's last verdict
         // came (vx_split.pool_last_ns; a pool still working is estimated from
@@ -2327,7 +2348,7 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             }
             if (ok) {
                 const double v = std::clamp(err, -0.25 * first_span_ms, 0.5 * first_span_ms) * 1e-3;
-                c->split_lag_s = c->split_lag_n++ ? 0.5 * (c->split_lag_s + v) : v;
+                c->split_lag.add(v);
             }
         }
     }
@@ -3123,9 +3144,10 @@ void vx_tuning_fail_launch_after(vx_ctx* c, int64_t k) {
 void vx_tuning_verify_copy_stream(vx_ctx* c, int mode) {
     if (c) c->verify_copy_stream = mode ? 1 : 0;
 }
-void vx_tuning_split_rules(vx_ctx* c, int one_round, uint64_t round_cap, int lag) {
+void vx_tuning_split_rules(vx_ctx* c, int one_round, uint64_t round_cap, int lag, int learn) {
     if (!c) return;
     c->split_lag_on = lag ? 1 : 0;
+    c->split_learn = learn ? 1 : 0;
     c->split_one_round = one_round == 2 ? 2 : one_round ? 1 : 0;
     c->split_round_cap = round_cap;
 }
