@@ -358,8 +358,12 @@ void vx_split_done(vx_split* s, uint64_t pieces);
 uint64_t vx_split_boundary(const vx_split* s);
 /* The engine's side: verifies the pieces it claims from s (always the top of
  * the range, contiguous) with resumable chunk rounds, while the caller's pool
- * runs vx_split_claim on its own threads; returns when its pieces are done,
- * possibly while the pool still works.  matched_out has end - first bytes
+ * runs vx_split_claim on its own threads; returns when its pieces are done.
+ * If the pool has reported verdicts and is still working then, the engine
+ * waits for it (polling, at most 3x its estimated remaining time + 50 ms) to
+ * learn how far the two finish times strayed, for the next call's first
+ * group; a pool that has reported nothing yet is not waited for, so a caller
+ * may also run its pool after this returns.  matched_out has end - first bytes
  * (matched_out[k] for piece first + k); the engine writes only its own
  * pieces' entries, the pool writes the others.  Returns the number of the
  * engine's pieces that hit an I/O error (>= 0), or a VX_E* code: then the

@@ -82,13 +82,14 @@ size_t vx_tuning_chunk_schedule(uint64_t L, uint64_t C, int head, int tail, uint
  * stop and (was, may be NULL) the stop before, so the pieces taken are
  * [returned, *was) (host-only). */
 uint64_t vx_tuning_split_take_tail(struct vx_split* s, uint64_t k, uint64_t* was);
-/* The last vx_verify_files_split call's decisions, one row of 12 doubles per
+/* The last vx_verify_files_split call's decisions, one row of 13 doubles per
  * round it formed: ms since the call's start, the pool's rate (pieces/s), the
  * engine's intake rate (B/s), its chain per 64-byte block (ns), the predicted
  * remaining ms of the engine and of the pool with the group taken, unclaimed
  * pieces, the group taken, active lanes, the pool's finished pieces, the
- * decision mode (0 later round, 1 first, 2 forced) and whether both sides'
- * rates were measured.  Writes up to max rows; returns the row count. */
+ * decision mode (0 later round, 1 first, 2 forced), whether both sides'
+ * rates were measured, and the learned lag (ms) inside the engine's time.
+ * Writes up to max rows; returns the row count. */
 size_t vx_tuning_last_split(const struct vx_ctx* ctx, double* out, size_t max);
 
 int vx_sha1_device_uniform_variant(const void* d_base, uint64_t stride, uint32_t len, uint32_t n, void* d_digests,

@@ -28,14 +28,14 @@ import oracle  # noqa: E402
 from vortex_amd.hash_pool import HashPool, plan_verify_split  # noqa: E402
 
 COLS = ("t_ms", "pool_rate", "engine_rate", "block_ns", "t_engine_ms", "t_pool_ms", "unclaimed", "group", "lanes",
-        "pool_done", "mode", "measured")
+        "pool_done", "mode", "measured", "lag_ms")
 
 
 def decisions(pool):
     n = pool.lib.vx_tuning_last_split(pool._h, None, 0)
-    buf = (ctypes.c_double * (12 * max(1, n)))()
+    buf = (ctypes.c_double * (len(COLS) * max(1, n)))()
     pool.lib.vx_tuning_last_split(pool._h, buf, n)
-    return [{k: round(buf[12 * i + j], 4) for j, k in enumerate(COLS)} for i in range(n)]
+    return [{k: round(buf[len(COLS) * i + j], 4) for j, k in enumerate(COLS)} for i in range(n)]
 
 
 def main():

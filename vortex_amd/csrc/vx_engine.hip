@@ -215,6 +215,7 @@ struct vx_ctx {
         double t_ms, pool_rate, engine_rate, block_ns, t_engine_ms, t_pool_ms;
         uint64_t unclaimed, group, lanes, pool_done;
         uint32_t mode, measured;
+        double lag_ms;  // the learned lag in t_engine_ms
     };
     std::vector<SplitDecision> last_split;
     // What earlier split calls measured, the next call's cold start: the
@@ -223,8 +224,11 @@ struct vx_ctx {
     // and the pool's bytes/s per thread beside the engine (0 = none yet).
     // Each keeps the last kLearn calls' samples: the next call uses their
     // median (split_learn 1, default), so one call slowed by a host stall
-    // does not move the next call's first group; split_learn 0 (test build)
-    // uses the running mean instead (each call weighted 1/2).
+    // does not move the next call's first group — and for the intake their
+    // largest: a stall slows the pool as much as the engine's reads, and the
+    // pool's side starts from its own rate alone, so the engine's starts from
+    // its unstalled one too.  split_learn 0 (test build) uses the running mean
+    // instead (each call weighted 1/2).
     struct Learned {
         static constexpr uint32_t kLearn = 5;
         double ring[kLearn] = {}, mean = 0;
@@ -234,6 +238,7 @@ struct vx_ctx {
             ring[n++ % kLearn] = x;
         }
         bool any() const { return n > 0; }
+        double top() const { return *std::max_element(ring, ring + std::min(n, kLearn)); }
         double get(int median) const {
             if (!median) return mean;
             double v[kLearn];
@@ -2027,7 +2032,7 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
         if (!*measured && !cold && mode == 0) return 0;
         if (windowed) last_p = p;
         const double rin = in_n >= 2 && in_ms > 0 ? in_bytes / (in_ms * 1e-3)
-                           : c->split_rin.any()   ? c->split_rin.get(c->split_learn)
+                           : c->split_rin.any()   ? (c->split_learn ? c->split_rin.top() : c->split_rin.get(0))
                                                   : kPcieRate;
         double bns = c->split_bns.any() ? c->split_bns.get(c->split_learn) : kChainBlock * 1e9;
         if (!block_ns.empty()) {
@@ -2108,7 +2113,7 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
         c->last_split.push_back(vx_ctx::SplitDecision{
             ((double)vx_files::Readers::now_ns() - (double)c->verify_t0_ns) * 1e-6, p, rin, bns,
             t_engine(lo) * 1e3, t_pool(lo) * 1e3, unclaimed, lo, (uint64_t)act.size(), done, (uint32_t)mode,
-            *measured ? 1u : 0u});
+            *measured ? 1u : 0u, lag_used * 1e3});
         return lo;
     };
 
@@ -2332,19 +2337,31 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             double err = end_ms - first_end_ms;
             bool ok = true;
             if (pool_threads > 0) {
-                const uint64_t w = __atomic_load_n(&sp->word, __ATOMIC_ACQUIRE);
-                const uint64_t head = w & 0xffffffffull, stop = w >> 32;
-                const uint64_t done = __atomic_load_n(&sp->pool_done, __ATOMIC_ACQUIRE);
-                const uint64_t last_ns = __atomic_load_n(&sp->pool_last_ns, __ATOMIC_ACQUIRE);
-                const uint64_t claimed = head - first, unclaimed = stop > head ? stop - head : 0;
-                double pool_end_ms = -1;
-                if (!unclaimed && done >= claimed && last_ns)
-                    pool_end_ms = ((double)last_ns - (double)c->verify_t0_ns) * 1e-6;
-                else if (last_p > 0)
-                    pool_end_ms = rel_ms(vx_files::Readers::now_ns()) +
-                                  (0.5 * (double)(claimed - std::min(done, claimed)) + (double)unclaimed) / last_p * 1e3;
-                ok = pool_end_ms > 0 && first_pool_end_ms > 0;
-                err -= pool_end_ms - first_pool_end_ms;
+                // A pool still verifying its last pieces is waited for (polled,
+                // at most 3x their estimated time + 50 ms): estimating its end
+                // instead would miss the stalls that come after the engine's,
+                // while counting those before it, and bias the lag up.  A pool
+                // that has reported nothing is not waited for.
+                uint64_t head = 0, stop = 0, done = 0, last_ns = 0;
+                auto load = [&] {
+                    const uint64_t w = __atomic_load_n(&sp->word, __ATOMIC_ACQUIRE);
+                    head = w & 0xffffffffull, stop = w >> 32;
+                    done = __atomic_load_n(&sp->pool_done, __ATOMIC_ACQUIRE);
+                    last_ns = __atomic_load_n(&sp->pool_last_ns, __ATOMIC_ACQUIRE);
+                };
+                auto busy = [&] { return stop > head || done < head - first; };
+                load();
+                if (busy() && done > 0 && last_p > 0) {
+                    const double left = 0.5 * (double)(head - first - std::min(done, head - first)) +
+                                        (double)(stop > head ? stop - head : 0);
+                    const uint64_t until = vx_files::Readers::now_ns() + (uint64_t)((3.0 * left / last_p + 0.05) * 1e9);
+                    while (busy() && vx_files::Readers::now_ns() < until) {
+                        std::this_thread::sleep_for(std::chrono::microseconds(200));
+                        load();
+                    }
+                }
+                ok = !busy() && last_ns && first_pool_end_ms > 0;
+                if (ok) err -= ((double)last_ns - (double)c->verify_t0_ns) * 1e-6 - first_pool_end_ms;
             }
             if (ok) {
                 const double v = std::clamp(err, -0.25 * first_span_ms, 0.5 * first_span_ms) * 1e-3;
@@ -3167,10 +3184,10 @@ size_t vx_tuning_last_split(const vx_ctx* c, double* out, size_t max) {
     const size_t k = std::min(max, c->last_split.size());
     for (size_t i = 0; i < k && out; ++i) {
         const auto& d = c->last_split[i];
-        const double row[12] = {d.t_ms, d.pool_rate, d.engine_rate, d.block_ns, d.t_engine_ms, d.t_pool_ms,
+        const double row[13] = {d.t_ms, d.pool_rate, d.engine_rate, d.block_ns, d.t_engine_ms, d.t_pool_ms,
                                 (double)d.unclaimed, (double)d.group, (double)d.lanes, (double)d.pool_done,
-                                (double)d.mode, (double)d.measured};
-        std::memcpy(out + 12 * i, row, sizeof row);
+                                (double)d.mode, (double)d.measured, d.lag_ms};
+        std::memcpy(out + 13 * i, row, sizeof row);
     }
     return c->last_split.size();
 }
