@@ -2329,8 +2329,8 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
         if (last_p > 0 && pool_threads > 0) c->split_pool_thread_rate.add(last_p * (double)pl / pool_threads);
         // The lag: how much later than predicted the engine's last kernel
         // ended, less how much later than predicted the pool's last verdict
-        // came (vx_split.pool_last_ns; a pool still working is estimated from
-        // its pace), both against the first group's decision.
+        // came (vx_split.pool_last_ns), both against the first group's
+        // decision.
         double end_ms = -1;
         for (const auto& r : c->last_rounds) end_ms = std::max(end_ms, r.kernel_end_ms);
         if (anchored && !later_group && engines == 1 && first_end_ms > 0 && end_ms > 0 && first_span_ms > 0) {
