@@ -291,3 +291,58 @@ def test_split_one_chunk_pieces(built, gpu, tmp_path, one_round, cap):
                     assert max(r["lanes"] for r in pool.last_verify_rounds()) <= 1024
         finally:
             pool.lib.vx_tuning_split_rules(pool._h, 1, 64 << 20, 1, 1)
+
+
+def test_split_engine_returns_when_the_pool_stalls(built, gpu, tmp_path):
+    """The engine waits for a pool still finishing its last pieces only for a
+    bounded time (vx_hash.h): a pool that reports one verdict and then holds
+    two claimed pieces without finishing them does not keep the engine's call
+    from returning.  The engine's verdicts, and the pool's once it finishes
+    what it held and claims what the engine left, match the pool
+    restatement's."""
+    import time
+
+    from vortex_amd.hash_pool import HashPool, Split
+
+    pl, n = 1 << 20, 200
+    paths, sizes, exp = _files(tmp_path, pl, [n * pl - 4321], 83)
+    with open(paths[0], "r+b") as f:  # a damaged piece on the engine's side
+        f.seek(150 * pl + 9)
+        b = f.read(1)
+        f.seek(150 * pl + 9)
+        f.write(bytes([b[0] ^ 0x20]))
+    want = oracle.pool_verify_files(paths, sizes, pl, exp, threads=4)
+    pool = HashPool(pl, slots=3, slot_bytes=64 << 20)
+    for rep in range(2):  # the second call starts from the first's learned state
+        sp = Split(0, n, cpu_threads=2, cpu_thread_rate=2e9)
+        held, release = [], threading.Event()
+
+        def stalled_pool():
+            for _ in range(3):
+                held.append(sp.claim())
+            i = held.pop(0)
+            sp.matched[i] = b"\x01" if want[i] else b"\x00"
+            sp.done(1)
+            release.wait(30)
+
+        th = threading.Thread(target=stalled_pool)
+        th.start()
+        while len(held) < 2:
+            time.sleep(0.001)
+        try:
+            t0 = time.perf_counter()
+            bad = pool.verify_files_split(paths, sizes, pl, exp, sp, io_threads=4)
+            took = time.perf_counter() - t0
+        finally:
+            release.set()
+        th.join()
+        assert took < 5.0, took
+        b = sp.boundary
+        assert 3 <= b < n and bad == 0, (rep, b)
+        # the caller's pool finishes what it held and claims what is left
+        rest = held + [i for i in iter(sp.claim, -1)]
+        assert sorted(rest) == [1, 2] + list(range(3, b)), (rep, b)
+        for i in rest:
+            sp.matched[i] = b"\x01" if want[i] else b"\x00"
+        assert sp.verdicts() == want, rep
+    pool.close()
