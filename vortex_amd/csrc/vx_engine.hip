@@ -2024,6 +2024,19 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
         // deciding so until the rates are in, rather than draining the pipeline.
         const bool cold = mode == 1 || (mode == 0 && one_round && !*measured);
         if (cold && pool_threads > 0) p = std::max(p, pool_rate0);
+        // With the engine idle (mode 2), a pool that has finished nothing for
+        // two of its piece times (at least the window) while pieces are still
+        // unclaimed is held up — vortex's rayon pool also hashes downloads —
+        // so it counts as stopped and the engine takes what it can, instead
+        // of leaving the rest to it.
+        if (mode == 2 && pool_threads > 0 && unclaimed > 0) {
+            const uint64_t win = std::max<uint64_t>(kPoolWindowNs, (uint64_t)(2e9 * (double)pl / thread_rate0));
+            for (size_t k = pool_samples.size() - 1; k-- > 0;)  // (the last sample is this call's)
+                if (now - pool_samples[k].first >= win) {
+                    if (pool_samples[k].second == done) p = 0;
+                    break;
+                }
+        }
         // pieces the pool holds count half done
         const double in_hand = 0.5 * ((double)(head - first) - (double)std::min<uint64_t>(done, head - first));
         // The engine's chain per block is a property of the kernel, known within
@@ -2065,7 +2078,8 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             }
         }
         const std::vector<uint64_t>& js = mode == 1 ? sched_ramp : sched_plain;
-        lag_used = mode == 1 && c->split_lag_on && c->split_lag.any() ? c->split_lag.get(c->split_learn) : 0.0;
+        // (the lag from three calls on: the median of one or two is their noise)
+        lag_used = mode == 1 && c->split_lag_on && c->split_lag.n >= 3 ? c->split_lag.get(c->split_learn) : 0.0;
         // Each round costs max(its bytes over the intake, its chain), copies
         // overlapping the previous round's kernel; after the last copy, the
         // last kernel's chain; before the first, the first round's read.
