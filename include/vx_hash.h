@@ -363,7 +363,10 @@ uint64_t vx_split_boundary(const vx_split* s);
  * waits for it (polling, at most 3x its estimated remaining time + 50 ms) to
  * learn how far the two finish times strayed, for the next call's first
  * group; a pool that has reported nothing yet is not waited for, so a caller
- * may also run its pool after this returns.  matched_out has end - first bytes
+ * may also run its pool after this returns.  With nothing in flight, the
+ * engine takes the unclaimed pieces itself when the pool has finished none
+ * for a while (two of its piece times, at least 4 ms): a pool busy elsewhere
+ * does not leave them waiting.  matched_out has end - first bytes
  * (matched_out[k] for piece first + k); the engine writes only its own
  * pieces' entries, the pool writes the others.  Returns the number of the
  * engine's pieces that hit an I/O error (>= 0), or a VX_E* code: then the
