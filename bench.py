@@ -770,6 +770,11 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 11):
             # alone (all threads) as references, so a box's drift lands on all of them alike.
             cfgs = [(first, io_t, pool_t) for first in points] + [(0, threads, threads), (n, threads, threads)]
             by_cfg = {c: [] for c in cfgs}
+            # The balanced split's first group starts from what the last split calls on
+            # the context measured: three untimed calls first, as a
+            # long-lived context has them (keep one context)
+            for _ in range(3):
+                assert balanced_call(pool, [path], [total], n, pl, exp, io_t, pool_t, rate)["ok"]
             bal = []  # the self-balancing split (no plan), in the same alternation
             for _ in range(split_reps):
                 for c in cfgs:
@@ -866,8 +871,8 @@ def reverify_leg(reps: int = 5, cold_reps: int = 3, split_reps: int = 11):
                   "sample": f"the warm file shared by the engine and the CPU pool restatement (vortex's par_iter "
                             f"stand-in, 3/4 of the {threads} threads) at once: balanced = vx_verify_files_split "
                             f"(the pool claims from the head, the engine sizes its groups from the rates it "
-                            f"measures); fixed points = vx_verify_files_range over [first, {n}) with the pool on "
-                            f"[0, first), first = vx_plan_verify_split's {split['plan']['gpu_first']} and 10 % "
+                            f"measures; after 3 untimed calls); fixed points = vx_verify_files_range over "
+                            f"[first, {n}) with the pool on [0, first), first = vx_plan_verify_split's {split['plan']['gpu_first']} and 10 % "
                             f"fewer / more GPU pieces; engine readers at half the threads; alternating call by "
                             f"call with the GPU alone and the pool alone (gpu_only / pool_only); median of "
                             f"{split_reps} per config; every verdict checked"})
