@@ -248,7 +248,10 @@ struct vx_ctx {
             return k % 2 ? v[k / 2] : 0.5 * (v[k / 2 - 1] + v[k / 2]);
         }
     };
-    Learned split_rin, split_bns, split_pool_thread_rate;
+    // [0]: calls over page-cached data, [1]: over uncached data (O_DIRECT
+    // reads; the disk, not PCIe, feeds the engine): one regime's figures
+    // would mislead the other's first group.
+    Learned split_rin[2], split_bns[2], split_pool_thread_rate[2];
     int split_learn = 1;
     // How much later the engine's last kernel ended than the first group's
     // T_engine said, less the same for the pool's last verdict and T_pool, in
@@ -256,7 +259,7 @@ struct vx_ctx {
     // start-up and the kernels trailing the copies, which the round model
     // leaves out), kept the same way; the next first group's T_engine adds
     // it.
-    Learned split_lag;
+    Learned split_lag[2];
     int split_lag_on = 1;  // 0: learned, not applied (vx_tuning_split_rules)
     // The file re-verify's chunk rounds put every H2D on this one stream (high
     // priority: its own hardware queue) and only kernels on the slot streams,
@@ -1826,7 +1829,7 @@ uint64_t split_take_tail(vx_split* s, uint64_t k, uint64_t expect = UINT64_MAX, 
 // the split (engines 1) the engine's pieces are the contiguous tail
 // [*lowest, end); beside other engines, the groups it took.
 int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n, uint32_t pl, uint64_t total,
-                 uint64_t C, uint64_t* lowest) {
+                 uint64_t C, uint64_t* lowest, int regime) {
     vx_ctx* c = fv.c;
     const uint64_t first = sp->first, end = sp->end, cnt = end - first;
     const uint64_t last_len = total - (n - 1) * (uint64_t)pl;
@@ -1925,7 +1928,7 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
     std::vector<std::pair<uint64_t, uint64_t>> mine;  // this engine's claims, [lo, hi), in claim order
     std::vector<std::pair<uint64_t, uint64_t>> pool_samples;  // (steady ns, pool_done) at each decision
     constexpr uint64_t kPoolWindowNs = 4000000;              // the pool's pace: its last 4 ms
-    const double thread_rate0 = c->split_pool_thread_rate.any() ? c->split_pool_thread_rate.get(c->split_learn)
+    const double thread_rate0 = c->split_pool_thread_rate[regime].any() ? c->split_pool_thread_rate[regime].get(c->split_learn)
                                 : sp->cpu_thread_rate > 0    ? sp->cpu_thread_rate
                                                              : 2.2e9;
     const double pool_rate0 = pool_threads * thread_rate0 / (double)pl;
@@ -2045,9 +2048,9 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
         if (!*measured && !cold && mode == 0) return 0;
         if (windowed) last_p = p;
         const double rin = in_n >= 2 && in_ms > 0 ? in_bytes / (in_ms * 1e-3)
-                           : c->split_rin.any()   ? (c->split_learn ? c->split_rin.top() : c->split_rin.get(0))
+                           : c->split_rin[regime].any() ? (c->split_learn ? c->split_rin[regime].top() : c->split_rin[regime].get(0))
                                                   : kPcieRate;
-        double bns = c->split_bns.any() ? c->split_bns.get(c->split_learn) : kChainBlock * 1e9;
+        double bns = c->split_bns[regime].any() ? c->split_bns[regime].get(c->split_learn) : kChainBlock * 1e9;
         if (!block_ns.empty()) {
             std::vector<double> b = block_ns;
             std::nth_element(b.begin(), b.begin() + b.size() / 2, b.end());
@@ -2079,7 +2082,7 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
         }
         const std::vector<uint64_t>& js = mode == 1 ? sched_ramp : sched_plain;
         // (the lag from three calls on: the median of one or two is their noise)
-        lag_used = mode == 1 && c->split_lag_on && c->split_lag.n >= 3 ? c->split_lag.get(c->split_learn) : 0.0;
+        lag_used = mode == 1 && c->split_lag_on && c->split_lag[regime].n >= 3 ? c->split_lag[regime].get(c->split_learn) : 0.0;
         // Each round costs max(its bytes over the intake, its chain), copies
         // overlapping the previous round's kernel; after the last copy, the
         // last kernel's chain; before the first, the first round's read.
@@ -2334,13 +2337,13 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             double bytes = 0;
             for (size_t k = a + 1; k <= b && a < copy_ends.size(); ++k) bytes += (double)copy_ends[k].bytes;
             const double ms = a < b ? copy_ends[b].end_ms - copy_ends[a].end_ms : 0.0;
-            if (ms > 0 && bytes > 0) c->split_rin.add(bytes / (ms * 1e-3));
+            if (ms > 0 && bytes > 0) c->split_rin[regime].add(bytes / (ms * 1e-3));
         }
         if (!block_ns.empty()) {
             std::nth_element(block_ns.begin(), block_ns.begin() + block_ns.size() / 2, block_ns.end());
-            c->split_bns.add(block_ns[block_ns.size() / 2]);
+            c->split_bns[regime].add(block_ns[block_ns.size() / 2]);
         }
-        if (last_p > 0 && pool_threads > 0) c->split_pool_thread_rate.add(last_p * (double)pl / pool_threads);
+        if (last_p > 0 && pool_threads > 0) c->split_pool_thread_rate[regime].add(last_p * (double)pl / pool_threads);
         // The lag: how much later than predicted the engine's last kernel
         // ended, less how much later than predicted the pool's last verdict
         // came (vx_split.pool_last_ns), both against the first group's
@@ -2379,7 +2382,7 @@ int verify_split(FileVerify& fv, vx_files::Readers& rd, vx_split* sp, uint64_t n
             }
             if (ok) {
                 const double v = std::clamp(err, -0.25 * first_span_ms, 0.5 * first_span_ms) * 1e-3;
-                c->split_lag.add(v);
+                c->split_lag[regime].add(v);
             }
         }
     }
@@ -2718,7 +2721,8 @@ static int64_t verify_files_impl(vx_ctx* c, const char* const* paths, const uint
                                 : C;
         c->last_verify.chunk_bytes = chunked ? Cv : 0;
         uint64_t lowest = end;
-        rc = sp        ? verify_split(fv, rd, sp, n_pieces, piece_length, total, Cv, &lowest)
+        const int regime = c->cfg.direct_io && dio.resident_fraction() < 0.5 ? 1 : 0;  // the split's learned figures
+        rc = sp        ? verify_split(fv, rd, sp, n_pieces, piece_length, total, Cv, &lowest, regime)
              : chunked ? verify_chunked(fv, rd, n_pieces, piece_length, total, first, end, Cv)
                        : verify_whole(fv, rd, n_pieces, piece_length, total, first, end);
 
